@@ -1,0 +1,239 @@
+"""Headline benchmark: scored (test-user, song) pairs/s of the ItemBasedModel.
+
+Workload (BASELINE.json configs[1], "C2"): ItemBasedModel over 500 train
+users / 10 test users / ~16.8k songs (synthetic), 1 MI355X.
+One step = one full pass of the hot path over the batch: stage 1 (neighbour
+weights), stage 2 (song-tile accumulation -> every (test user, unheard song)
+score written to HBM as fp32) and stage 3 (top-10 per test user) — what the
+reference's getItemBasedModel computes (MusicRecommender.scala MR:222-261),
+plus the recommendation list.
+
+Multi-GPU (one process per GPU, torchrun): weak scaling over test-user blocks —
+rank r scores test users [10r, 10r+10) of a 500 x 10N dataset over all songs
+(an exact partition of the model's pairs; no data-path collective). With
+``--shard songs`` the north star's song-range layout runs instead (every rank
+scores 10N test users on its song range, then one RCCL all-gather of the
+top-k lists + merge).
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the byte model.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (first: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from musicrecommendation_amd import synth  # noqa: E402
+from musicrecommendation_amd.engine import Engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+SCALA_PAR_PAIRS_PER_S = 508.0  # ibm par 500/10/16,785 = 330,385 ms (README.md:106)
+TEST_PER_GPU = 10
+
+
+def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
+    """SURVEY.md §8d byte model, split per kernel.
+    Per test user u with neighbours N(u) = ∪_{s2∈T(u)} L_tr(s2):
+      stage 1  12|T(u)| + 4 Σ_{s2∈T(u)} c_tr(s2)
+      stage 2  Σ_{v∈N(u)} (8 + 4|S(v)|) + 4 n_s + out_bytes (n_s − |T(u)|)
+      stage 3  12 k
+    """
+    n_s = ds.n_songs
+    tr_deg = np.diff(ds.tr_off)
+    trs_ptr = np.zeros(n_s + 1, dtype=np.int64)
+    np.cumsum(np.bincount(ds.tr_songs, minlength=n_s), out=trs_ptr[1:])
+    order = np.argsort(ds.tr_songs, kind="stable")
+    trs_users = np.repeat(np.arange(ds.n_train), tr_deg)[order]
+    c_tr = np.diff(trs_ptr)
+    b1 = b2 = 0
+    for u in range(ds.n_test):
+        T = ds.te_songs[ds.te_off[u]:ds.te_off[u + 1]]
+        nb = np.unique(np.concatenate([trs_users[trs_ptr[s]:trs_ptr[s + 1]] for s in T])) if T.size else []
+        b1 += 12 * T.size + 4 * int(c_tr[T].sum())
+        b2 += int(np.sum(8 + 4 * tr_deg[nb])) + 4 * n_s + out_bytes * (n_s - T.size)
+    return {"neighbours": b1, "score": b2, "merge": 12 * k * ds.n_test}
+
+
+def cpu_baseline(ds, model: str, seconds: float):
+    """Literal restatement of getItemBasedModelP (oracle/literal.c, string ids,
+    linear contains, pthreads over songs x users like MR:119-125) timed on a
+    bounded block of the s-major pair enumeration."""
+    from oracle import native
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    tr, te, _ = native.dataset_lines(ds)
+    li = native.LiteralInputs(tr, te)
+    total = ds.n_songs * ds.n_test
+    n = 16 * threads
+    t0 = time.perf_counter()
+    li.model(model, threads=threads, pair_lo=0, pair_hi=n)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    n = int(min(total, max(n, n * seconds / dt)))
+    t0 = time.perf_counter()
+    _, emitted = li.model(model, threads=threads, pair_lo=0, pair_hi=n)
+    dt = time.perf_counter() - t0
+    return {
+        "value": emitted / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+        "sample": f"oracle/literal.c {model}: first {n} of {total} (song, user) pairs of the C2 "
+                  f"enumeration ({emitted} scored), {dt:.1f} s",
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--model", default="ibm", choices=["ibm", "ubm"])
+    ap.add_argument("--shard", default="users", choices=["users", "songs"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per score-kernel launch measured by rocprofv3 PMC (profiles/)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n_tr, n_te, _seed, _t = synth.CONFIGS[args.config]
+    if args.shard == "users":
+        full = synth.config(args.config, n_test=n_te * world).dataset()
+        ds = full.subset_test_users(rank * n_te, (rank + 1) * n_te)
+        eng = Engine(ds, device=local, out_dtype="f32", topk=10, time_kernels=True)
+        pairs_rank = ds.n_pairs()
+
+        def step():
+            eng.run(args.model)
+
+        def drain():
+            eng.sync()
+    else:
+        from musicrecommendation_amd.sharding import SongShardScorer
+
+        full = ds = synth.config(args.config, n_test=n_te * world).dataset()
+        scorer = SongShardScorer(ds, rank, world, local, topk=10, out_dtype="f32", time_kernels=True)
+        eng = scorer.engine
+        heard = ds.heard_mask()[:, eng.song_lo:eng.song_hi]
+        pairs_rank = int(heard.size - heard.sum())
+
+        def step():
+            scorer.step(args.model)
+
+        def drain():
+            eng.sync()
+
+    for _ in range(args.warmup):
+        step()
+    drain()
+    for kname in ("neighbours", "score", "merge"):
+        eng.kernel_times(kname, reset=True)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    kt = {k: eng.kernel_times(k) for k in ("neighbours", "score", "merge")}
+    stats = torch.tensor([elapsed, float(pairs_rank)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        t_max = stats[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed_max, pairs_all = float(t_max.item()), float(tot.item())
+    else:
+        elapsed_max, pairs_all = elapsed, float(pairs_rank)
+
+    if rank == 0:
+        value = pairs_all * args.steps / elapsed_max
+        ab = algorithmic_bytes(ds, 4, 10)
+        avg_us = {k: (kt[k][1] / kt[k][0] * 1e3 if kt[k][0] else None) for k in kt}
+        dom = max(("neighbours", "score", "merge"), key=lambda k: avg_us[k] or 0.0)
+        achieved = ab[dom] / (avg_us[dom] * 1e-6) / 1e9
+        step_bytes = sum(ab.values())
+        traffic = args.traffic_bytes
+        # quality companions on the last step's outputs (host-side, untimed)
+        from musicrecommendation_amd import evaluation
+
+        if args.shard == "users":
+            songs, _sc, _k = eng.topk()
+            map10 = evaluation.map_at_k(songs, ds, 10)
+            ref_map = evaluation.threshold_map(eng.dense().astype(np.float64), ds)
+        else:
+            s_, _k = scorer.topk()
+            map10 = evaluation.map_at_k(s_, ds, 10)
+            ref_map = None
+        line = {
+            "metric": "scored (test-user,song) pairs/sec, ItemBasedModel, 1/2/4/8 MI355X + mAP@10"
+            if args.model == "ibm" else "scored (test-user,song) pairs/sec, UserBasedModel",
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / SCALA_PAR_PAIRS_PER_S if args.model == "ibm" else None,
+            "dtype": "int64",
+            "data": "synthetic (seeded Zipf/lognormal Taste-Profile-shaped triplets, SURVEY.md §8d)",
+            "config": {
+                "workload": f"{args.config}: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} "
+                            f"{n_tr} train / {n_te} test per GPU / {full.n_songs} songs, "
+                            f"fp32 dense scores + top-10, shard={args.shard}",
+                "n_train": n_tr, "n_test": full.n_test, "n_songs": full.n_songs,
+                "pairs_per_step": pairs_all, "parallelism": f"{args.shard}{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": f"k_score ({dom})" if dom == "score" else dom,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": ab[dom],
+                "avg_launch_us": avg_us[dom],
+            },
+            "kernels_avg_us": avg_us,
+            "step_algorithmic_bytes": step_bytes,
+            "step_GBps": step_bytes / (elapsed_max / args.steps) / 1e9,
+            "mAP@10": map10,
+            "ref_threshold_mAP": ref_map,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(ds, args.model, args.cpu_baseline_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+/*
+ * mr_engine.h — C ABI of the MI355X collaborative-filtering similarity engine.
+ *
+ * This is the drop-in boundary for the reference's scoring hot path
+ * (alberto-paparella/MusicRecommendation, paths relative to the reference root;
+ * MR = src/main/scala/music_recommandation/MusicRecommender.scala):
+ *
+ *   reference                                       replaced by
+ *   ----------------------------------------------  -------------------------------------------
+ *   extractData / songs / songsToUsersMap MR:26-62  mr_corpus_from_tsv, mr_corpus_dataset (host)
+ *   importTestLabels MR:70-91                       mr_corpus_from_tsv (labels CSR)
+ *   getModel(rank) MR:105-111, getModelP MR:119-125 mr_run / mr_score_dense (batched, all pairs)
+ *   UBM cosineSimilarity+rank MR:140-166            model = MR_UBM
+ *   IBM cosineSimilarity+rank MR:230-257            model = MR_IBM
+ *   getUserBasedModel(P) MR:132-215                 mr_score_dense(ctx, MR_UBM, ...)
+ *   getItemBasedModel(P) MR:222-307                 mr_score_dense(ctx, MR_IBM, ...)
+ *   Spark song partition getItemBasedModel2        mr_options.song_lo/song_hi (song-range shard)
+ *     distributed.scala:477-479
+ *
+ * The reference has no FFI: its only plug point is the private closure
+ * `rank: (String,String) => Double` (MR:105). A per-pair foreign call is ruled
+ * out (3.85e9 pairs at full scale), so the boundary is the batched model: the
+ * caller hands over interned CSR arrays once (mr_load) and receives every
+ * (test user, song) score of the model in one call.
+ *
+ * Conventions (all plain C; no C++ or torch types cross this boundary):
+ *  - Ids are dense int32. Songs are numbered in lexicographic order of their
+ *    string id, users likewise (the driver's sort key, main.scala:57-59).
+ *  - Return value 0 = MR_OK; negative = error; mr_last_error() describes the
+ *    last error of the calling thread. Nothing here calls exit()/abort()
+ *    (the reference's System.exit at MR:326 etc. becomes an error code).
+ *  - Ownership: the caller owns every host buffer it passes; mr_load COPIES.
+ *    The context owns its device memory and its HIP stream.
+ *  - Threading: one context is driven by one host thread at a time; calls on
+ *    different contexts are independent. mr_run is asynchronous on the
+ *    context's stream; every other compute call is synchronous.
+ */
+#ifndef MR_ENGINE_H
+#define MR_ENGINE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define MR_OK          0
+#define MR_E_INVALID  -1 /* bad shape, unsorted/duplicate CSR, train∩test users, bad option */
+#define MR_E_HIP      -2 /* HIP runtime error (no device, launch failure, ...)           */
+#define MR_E_OOM      -3 /* device or host allocation failed                               */
+#define MR_E_STATE    -4 /* call out of order (e.g. mr_run before mr_load)                 */
+#define MR_E_IO       -5 /* file could not be opened/read                                  */
+#define MR_E_PARSE    -6 /* malformed TSV line (reference: scala.MatchError, MR:34)         */
+
+/* ---- models ------------------------------------------------------------ */
+#define MR_UBM 0 /* UserBasedModel: MR:140-166 */
+#define MR_IBM 1 /* ItemBasedModel: MR:230-257 */
+
+/* ---- dense output element type ------------------------------------------ */
+#define MR_OUT_F32 0
+#define MR_OUT_F64 1
+
+/*
+ * Interned dataset, the engine's input. Mirrors the maps built by
+ * extractData (MR:26-62). All CSR column lists are sorted ascending and
+ * duplicate-free; the *_len arrays keep the reference's duplicate-counting
+ * `.length` semantics (MR:147, MR:237).
+ *
+ *  n_train_users  = |trainUsers|                                (MR:55)
+ *  n_test_users   = |testUsers|                                 (MR:56)
+ *  n_songs        = |songs| = distinct songs of train ∪ test    (MR:58)
+ *  tr_off/tr_songs: train user v -> distinct songs S(v)         (trainUsersToSongsMap)
+ *  te_off/te_songs: test user u  -> distinct visible songs T(u) (testUsersToSongsMap)
+ *  song_count[s]  = songsToUsersMap(s).length: train AND test lines, dups counted (MR:60-62, MR:237)
+ *  tr_len[v]      = trainUsersToSongsMap(v).length, dups counted (MR:147)
+ *  te_len[u]      = testUsersToSongsMap(u).length, dups counted  (MR:147)
+ * Train and test users must be disjoint (dataExtraction.ipynb:149,301); the
+ * engine checks what it can (every test user has >=1 visible song, counts
+ * are consistent with the CSR) and returns MR_E_INVALID otherwise.
+ * The song -> train-users transpose is built by mr_load itself.
+ */
+typedef struct mr_dataset {
+  int32_t n_train_users;
+  int32_t n_test_users;
+  int32_t n_songs;
+  int32_t reserved0;
+  const int64_t* tr_off;     /* [n_train_users + 1] */
+  const int32_t* tr_songs;   /* [tr_off[n_train_users]] */
+  const int64_t* te_off;     /* [n_test_users + 1] */
+  const int32_t* te_songs;   /* [te_off[n_test_users]] */
+  const int32_t* song_count; /* [n_songs] */
+  const int32_t* tr_len;     /* [n_train_users] */
+  const int32_t* te_len;     /* [n_test_users] */
+} mr_dataset;
+
+typedef struct mr_options {
+  int32_t device;      /* HIP device ordinal (default 0) */
+  int32_t frac_bits;   /* fixed-point fraction bits F of the int64 accumulators (default 32, 8..40) */
+  int32_t song_lo;     /* first song id of this context's shard (default 0) */
+  int32_t song_hi;     /* one past the last song id; <= 0 means n_songs (default 0) */
+  int32_t block_songs; /* songs per LDS accumulator tile; 0 = auto (multiple of 256, <= 16384) */
+  int32_t out_dtype;   /* MR_OUT_F32 (default) or MR_OUT_F64 for the dense model */
+  int32_t topk;        /* k of the per-test-user recommendation list (0 = off, <= 64; default 10) */
+  int32_t dense;       /* 1 (default) = write the dense model; 0 = top-k only */
+  int32_t time_kernels;/* 1 = record HIP events around each kernel in mr_run (see mr_kernel_times) */
+  int32_t reserved[7];
+} mr_options;
+
+typedef struct mr_ctx mr_ctx;
+
+/* Fill *opt with defaults. */
+int mr_options_default(mr_options* opt);
+
+/* Create a context on opt->device (its own HIP stream). */
+int mr_create(const mr_options* opt, mr_ctx** out);
+int mr_destroy(mr_ctx* ctx);
+
+/* Validate, copy to the device and build the device-side indexes. */
+int mr_load(mr_ctx* ctx, const mr_dataset* d);
+
+/* Shard geometry after mr_load: [*song_lo, *song_hi) and the number of
+ * test users. The dense model of this context is n_te x (song_hi - song_lo). */
+int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
+
+/*
+ * Score every (test user, song) pair of the shard for `model`, leaving the
+ * results in device buffers (asynchronous on the context stream):
+ *  dense[u][s - song_lo] = rank(u, s) for s not in T(u), NaN for s in T(u)
+ *      (the reference emits no pair for heard songs, MR:109);
+ *  topk[u][0..k)  = the k unheard songs of the shard with the highest score,
+ *      ordered by (score desc, song id asc); the fixed-point key makes this
+ *      order identical for any shard count. Missing entries: song -1.
+ */
+int mr_run(mr_ctx* ctx, int model);
+int mr_sync(mr_ctx* ctx);
+
+/* Device pointers of the last mr_run's outputs (valid until the next
+ * mr_run/mr_load/mr_destroy). Any pointer may be NULL. */
+int mr_device_outputs(const mr_ctx* ctx, void** dense, int32_t** topk_songs,
+                      int64_t** topk_keys, double** topk_scores);
+
+/* Synchronous convenience calls: run + copy to caller-allocated host buffers.
+ * out: n_te * (song_hi - song_lo) elements of the context's out_dtype. */
+int mr_score_dense(mr_ctx* ctx, int model, void* out);
+/* songs/scores: n_te * k; keys (may be NULL): fixed-point sort keys. */
+int mr_topk(mr_ctx* ctx, int model, int k, int32_t* songs, double* scores, int64_t* keys);
+
+/* Copy the last mr_run's outputs to host buffers (synchronous). */
+int mr_copy_dense(mr_ctx* ctx, void* out);
+int mr_copy_topk(mr_ctx* ctx, int32_t* songs, double* scores, int64_t* keys);
+/* Same, into DEVICE buffers of the context's GPU (e.g. an all-gather send
+ * buffer owned by the caller); stream-ordered, returns after completion. */
+int mr_copy_topk_device(mr_ctx* ctx, int32_t* songs, int64_t* keys);
+
+/*
+ * Merge per-shard top-k lists (G shards, each n_te x k, song ids global) into
+ * one n_te x k list by (key desc, song asc) — the exchange step of a
+ * song-sharded run after the all-gather. Host version (no GPU needed) and a
+ * device version that runs on the context stream over device pointers.
+ */
+int mr_topk_merge_host(int32_t n_shards, int32_t n_te, int32_t k,
+                       const int32_t* songs_in, const int64_t* keys_in, const double* scores_in,
+                       int32_t* songs_out, int64_t* keys_out, double* scores_out);
+int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
+                         const int32_t* songs_in, const int64_t* keys_in, const double* scores_in,
+                         int32_t* songs_out, int64_t* keys_out, double* scores_out);
+
+/* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
+ * (0 = neighbour weights, 1 = song-tile scoring, 2 = top-k merge) the number
+ * of timed launches and their summed device milliseconds; reset=1 clears. */
+int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
+
+/* HIP stream of the context (as void* = hipStream_t). */
+void* mr_stream(const mr_ctx* ctx);
+
+/* Thread-local description of the last error (never NULL). */
+const char* mr_last_error(void);
+
+/* ---- host ingest: TSV triplets -> interned corpus (extractData, MR:26-91) ---- */
+typedef struct mr_corpus mr_corpus;
+
+/*
+ * Parse `user \t song \t playcount` files (playcount ignored, MR:35) into an
+ * interned corpus. labels_path may be NULL. Songs = distinct songs of train ∪
+ * test (labels do not add songs, MR:79); ids are lexicographic.
+ * Malformed lines (not exactly 3 tab-separated fields) -> MR_E_PARSE.
+ */
+int mr_corpus_from_tsv(const char* train_path, const char* test_path,
+                       const char* labels_path, mr_corpus** out);
+/* Borrowed view of the corpus as an engine dataset (valid while the corpus lives). */
+int mr_corpus_dataset(const mr_corpus* c, mr_dataset* out);
+/* Test labels CSR over test users (songs of the labels file that are in
+ * `songs` get their id; label songs outside `songs` get ids >= n_songs,
+ * numbered lexicographically among themselves). n_label_songs counts the
+ * distinct label songs (= newSongs, MR:79). */
+int mr_corpus_labels(const mr_corpus* c, const int64_t** off, const int32_t** songs,
+                     int32_t* n_label_songs, int32_t* n_extra_songs);
+/* String ids (NUL-terminated, owned by the corpus). kind: 0 = song (ids
+ * 0..n_songs+n_extra_songs), 1 = train user, 2 = test user. */
+const char* mr_corpus_name(const mr_corpus* c, int32_t kind, int32_t id);
+int mr_corpus_free(mr_corpus* c);
+
+/* Library version string. */
+const char* mr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MR_ENGINE_H */

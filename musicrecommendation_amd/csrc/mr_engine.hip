@@ -1,0 +1,860 @@
+// mr_engine.hip — MI355X (gfx950) collaborative-filtering similarity engine.
+//
+// Replaces the per-pair scoring MapReduce of the reference
+// (src/main/scala/music_recommandation/MusicRecommender.scala, "MR"):
+//   getModel(rank)            MR:105-111   (all unheard (user, song) pairs)
+//   UBM cosine + rank         MR:140-166
+//   IBM cosine + rank         MR:230-257
+// by a two-stage sparse computation (SURVEY.md §0.1 "two-hop identity"):
+//   stage 1 (k_neighbours): per test user u, one weight per train neighbour v
+//       ibm: y_v = Σ_{s2 ∈ T(u) ∩ S(v)} q(s2),   q(s2) = rint(2^F / sqrt c(s2))
+//       ubm: o_v = |T(u) ∩ S(v)|,  q_v = rint(2^F · o_v / (sqrt|T(u)| · sqrt|S(v)|))
+//   stage 2 (k_score): per (u, song tile) an LDS int64 accumulator
+//       acc[s] = Σ_{v ∈ N(u), s ∈ S(v)} weight_v
+//       ibm: score = acc·2^-F / sqrt c(s);  ubm: score = acc·2^-F
+//     + dense write (NaN for heard songs, MR:109) + the tile's top-k candidates
+//   stage 3 (k_topk_merge): per test user, top-k over the tile candidates.
+// Integer accumulation is associative, so every launch geometry, shard count
+// and the CPU fixed-point oracle (oracle/fixedpoint.c) give bit-identical
+// scores and hence identical top-k order. Build with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "mr_engine.h"
+
+namespace {
+
+constexpr int kThreads = 256;            // 4 waves of 64
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxTopK = 64;
+constexpr int kMaxBlockSongs = 16384;    // 128 KiB of int64 accumulators (LDS is 160 KiB)
+constexpr int kMaxLdsTrainUsers = 16384; // stage-1 dense neighbour array in LDS (int64)
+constexpr long long kKeyNone = -1;       // valid keys are bit patterns of doubles >= 0
+
+thread_local std::string g_err = "no error";
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+}  // namespace
+
+namespace mr_host {
+// Error slot used by mr_host.cpp (same thread-local message as the device part).
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+}  // namespace mr_host
+
+namespace {
+
+#define MR_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(e_ == hipErrorOutOfMemory ? MR_E_OOM : MR_E_HIP, "%s failed: %s (%s:%d)", \
+                  #call, hipGetErrorString(e_), __FILE__, __LINE__);                   \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+
+// Block-wide exclusive scan of one int per thread (256 threads). `sbuf` holds kWaves ints.
+__device__ __forceinline__ int block_excl_scan(int x, int* total, int* sbuf) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) sbuf[w] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    int s = sbuf[i];
+    off += (i < w) ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + incl - x;
+}
+
+// Total order of recommendation candidates: score (key) descending, song ascending.
+__device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, int sb) {
+  return ka > kb || (ka == kb && sa < sb);
+}
+
+// Block-wide best candidate; every thread returns the same (key, song).
+__device__ __forceinline__ void block_best(long long& k, int& s, long long* sk, int* ss) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    long long ko = __shfl_xor(k, m, 64);
+    int so = __shfl_xor(s, m, 64);
+    if (cand_before(ko, so, k, s)) { k = ko; s = so; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sk[w] = k; ss[w] = s; }
+  __syncthreads();
+  k = sk[0]; s = ss[0];
+#pragma unroll
+  for (int i = 1; i < kWaves; ++i)
+    if (cand_before(sk[i], ss[i], k, s)) { k = sk[i]; s = ss[i]; }
+  __syncthreads();
+}
+
+// Top-k selection by repeated block argmax: round r picks the best candidate
+// strictly after round r-1's winner in the total order (candidates are
+// distinct songs, so no "taken" marks are needed). Load(i) -> (key, song);
+// key < 0 means "not a candidate".
+template <typename Load>
+__device__ __forceinline__ void block_select_topk(int n, int k, Load load, long long* out_key,
+                                                  int* out_song, long long* sk, int* ss) {
+  long long pk = LLONG_MAX;
+  int ps = -1;
+  int r = 0;
+  for (; r < k; ++r) {
+    long long bk = kKeyNone;
+    int bs = INT_MAX;
+    for (int i = threadIdx.x; i < n; i += kThreads) {
+      long long ck;
+      int cs;
+      load(i, ck, cs);
+      if (ck >= 0 && cand_before(pk, ps, ck, cs) && cand_before(ck, cs, bk, bs)) { bk = ck; bs = cs; }
+    }
+    block_best(bk, bs, sk, ss);
+    if (bk < 0) break;
+    if (threadIdx.x == 0) { out_key[r] = bk; out_song[r] = bs; }
+    pk = bk; ps = bs;
+  }
+  for (int i = r + threadIdx.x; i < k; i += kThreads) { out_key[i] = kKeyNone; out_song[i] = -1; }
+}
+
+// ---------------------------------------------------------------------------
+// stage 1: neighbour weights (one workgroup per test user, dense LDS array
+// over the train users). MR:140-149 (ubm numerator) / MR:230-239 (ibm).
+// ---------------------------------------------------------------------------
+struct NbrParams {
+  int n_tr;
+  int user0;                 // first test user of this launch
+  int cap;                   // neighbour-list capacity per user (= n_tr)
+  int frac_bits;
+  const long long* te_off;   // [n_te+1]
+  const int* te_songs;
+  const long long* trs_off;  // song -> train users CSR [n_s+1]
+  const int* trs_users;
+  const long long* q_song;   // ibm: rint(2^F / sqrt c(s))
+  const double* sqrt_tr;     // sqrt(|S(v)|) with duplicates (MR:147)
+  const double* sqrt_te;     // sqrt(|T(u)|) with duplicates
+  int* nbr_v;                // [batch][cap]
+  long long* nbr_q;          // [batch][cap]
+  int* nbr_cnt;              // [batch]
+};
+
+template <int MODEL>
+__global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
+  extern __shared__ unsigned long long smem[];
+  unsigned long long* Y = smem;                         // [n_tr]
+  long long* s_lo = reinterpret_cast<long long*>(Y + p.n_tr);  // [256] list start
+  long long* s_w = s_lo + kThreads;                     // [256] weight
+  int* s_pre = reinterpret_cast<int*>(s_w + kThreads);  // [257] exclusive prefix
+  int* s_scan = s_pre + kThreads + 1;                   // [kWaves]
+
+  const int bu = blockIdx.x;           // user within batch
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+  __syncthreads();
+
+  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  for (long long base = t0; base < t1; base += kThreads) {
+    const int n = (int)min((long long)kThreads, t1 - base);
+    int len = 0;
+    if (tid < n) {
+      const int s2 = p.te_songs[base + tid];
+      const long long lo = p.trs_off[s2];
+      len = (int)(p.trs_off[s2 + 1] - lo);
+      s_lo[tid] = lo;
+      s_w[tid] = (MODEL == MR_IBM) ? p.q_song[s2] : 1ll;
+    }
+    int total;
+    const int pre = block_excl_scan(len, &total, s_scan);
+    s_pre[tid] = pre;
+    if (tid == 0) s_pre[kThreads] = total;
+    __syncthreads();
+    // Flattened walk over the listener lists L_tr(s2), s2 in this chunk of T(u).
+    for (int i = tid; i < total; i += kThreads) {
+      int a = 0, b = n;  // find j with s_pre[j] <= i < s_pre[j+1]
+      while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (s_pre[m] <= i) a = m; else b = m;
+      }
+      const int v = p.trs_users[s_lo[a] + (i - s_pre[a])];
+      atomicAdd(&Y[v], (unsigned long long)s_w[a]);
+    }
+    __syncthreads();
+  }
+
+  // Compact the non-zero neighbours in train-user order.
+  const double two_f = ldexp(1.0, p.frac_bits);
+  const double rs_u = p.sqrt_te[u];
+  int* out_v = p.nbr_v + (size_t)bu * p.cap;
+  long long* out_q = p.nbr_q + (size_t)bu * p.cap;
+  int written = 0;
+  for (int v0 = 0; v0 < p.n_tr; v0 += kThreads) {
+    const int v = v0 + tid;
+    const unsigned long long y = (v < p.n_tr) ? Y[v] : 0ull;
+    const int flag = y != 0ull;
+    int total;
+    const int pos = block_excl_scan(flag, &total, s_scan);
+    if (flag) {
+      long long q;
+      if (MODEL == MR_IBM) {
+        q = (long long)y;
+      } else {
+        // cos_u = o / (sqrt|T(u)| * sqrt|S(v)|)  (MR:142-148), in fixed point.
+        const double c = (double)(long long)y / (rs_u * p.sqrt_tr[v]);
+        q = (long long)rint(c * two_f);
+      }
+      out_v[written + pos] = v;
+      out_q[written + pos] = q;
+    }
+    written += total;
+  }
+  if (tid == 0) p.nbr_cnt[bu] = written;
+}
+
+// ---------------------------------------------------------------------------
+// stage 2: per (song tile, test user) LDS accumulation + dense epilogue +
+// per-tile top-k candidates. MR:159-166 (ubm rank), MR:249-257 (ibm rank),
+// MR:105-111 (pair enumeration; heard songs get NaN instead of no pair).
+// ---------------------------------------------------------------------------
+struct ScoreParams {
+  int user0;
+  int song_lo, song_hi, width;   // shard [lo, hi), width = hi - lo
+  int block_songs, n_tiles;
+  int cap, frac_bits, topk, dense;
+  const long long* te_off;
+  const int* te_songs;
+  const int* tr_songs;           // train u -> s column ids
+  const int* blk_ptr;            // [n_tr][n_tiles+1] index into tr_songs
+  const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
+  const int* nbr_v;
+  const long long* nbr_q;
+  const int* nbr_cnt;
+  void* dense_out;               // [n_te][width] float or double
+  long long* cand_key;           // [batch][n_tiles][k]
+  int* cand_song;
+};
+
+template <int MODEL, typename OutT>
+__global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
+  extern __shared__ unsigned long long smem[];
+  const int bs = p.block_songs;
+  unsigned long long* acc = smem;                                   // [bs]
+  unsigned* heard = reinterpret_cast<unsigned*>(acc + bs);          // [bs/32]
+  long long* sk = reinterpret_cast<long long*>(heard + bs / 32);    // [kWaves]
+  int* ss = reinterpret_cast<int*>(sk + kWaves);                    // [kWaves]
+
+  const int tile = blockIdx.x;
+  const int bu = blockIdx.y;
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x;
+  const int blo = p.song_lo + tile * bs;
+  const int bhi = min(p.song_hi, blo + bs);
+  const int bw = bhi - blo;
+
+  for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
+  for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
+  __syncthreads();
+
+  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  for (long long i = t0 + tid; i < t1; i += kThreads) {
+    const int s = p.te_songs[i];
+    if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
+  }
+
+  const int cnt = p.nbr_cnt[bu];
+  const int* nv = p.nbr_v + (size_t)bu * p.cap;
+  const long long* nq = p.nbr_q + (size_t)bu * p.cap;
+  const int stride = p.n_tiles + 1;
+  for (int k = tid; k < cnt; k += kThreads) {
+    const int v = nv[k];
+    const unsigned long long q = (unsigned long long)nq[k];
+    const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+    const int a = bp[0], b = bp[1];
+    for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+  }
+  __syncthreads();
+
+  // Epilogue: scores -> dense row segment; keys stay in LDS for the top-k.
+  const double inv_f = ldexp(1.0, -p.frac_bits);
+  OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
+  for (int i = tid; i < bw; i += kThreads) {
+    const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+    double score = (double)(long long)acc[i] * inv_f;
+    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
+    if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+    acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
+  }
+  if (p.topk <= 0) return;
+  __syncthreads();
+  long long* ck = p.cand_key + ((size_t)bu * p.n_tiles + tile) * p.topk;
+  int* cs = p.cand_song + ((size_t)bu * p.n_tiles + tile) * p.topk;
+  block_select_topk(
+      bw, p.topk,
+      [&](int i, long long& key, int& song) {
+        key = (long long)acc[i];
+        song = blo + i;
+      },
+      ck, cs, sk, ss);
+}
+
+// ---------------------------------------------------------------------------
+// stage 3: top-k merge over lists. Element (u, l, r) of the input sits at
+// u*user_stride + l*list_stride + r. Used for the per-tile candidates of one
+// context and for the per-shard lists after the all-gather.
+// ---------------------------------------------------------------------------
+struct MergeParams {
+  int n_lists, k_in, k_out;
+  long long user_stride, list_stride;
+  const long long* keys;
+  const int* songs;
+  long long* out_keys;    // [n_users][k_out]
+  int* out_songs;
+  double* out_scores;     // may be null
+  long long out_user0;    // output row offset
+};
+
+__global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
+  __shared__ long long sk[kWaves];
+  __shared__ int ss[kWaves];
+  __shared__ long long wk[kMaxTopK];
+  __shared__ int ws[kMaxTopK];
+  const int bu = blockIdx.x;
+  const long long* keys = p.keys + (size_t)bu * p.user_stride;
+  const int* songs = p.songs + (size_t)bu * p.user_stride;
+  block_select_topk(
+      p.n_lists * p.k_in, p.k_out,
+      [&](int i, long long& key, int& song) {
+        const int l = i / p.k_in, r = i - l * p.k_in;
+        const size_t off = (size_t)l * p.list_stride + r;
+        key = keys[off];
+        song = songs[off];
+      },
+      wk, ws, sk, ss);
+  __syncthreads();
+  const size_t o = (size_t)(p.out_user0 + bu) * p.k_out;
+  for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
+    p.out_keys[o + r] = wk[r];
+    p.out_songs[o + r] = ws[r];
+    if (p.out_scores) p.out_scores[o + r] = wk[r] >= 0 ? __longlong_as_double(wk[r]) : (double)NAN;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+template <typename T>
+int dev_alloc(DevBuf<T>& b, size_t n) {
+  b.release();
+  if (n == 0) n = 1;
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&b.p), n * sizeof(T)));
+  b.n = n;
+  return MR_OK;
+}
+
+template <typename T>
+int dev_upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t st) {
+  int rc = dev_alloc(b, n);
+  if (rc) return rc;
+  if (n) MR_HIP(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, st));
+  return MR_OK;
+}
+
+}  // namespace
+
+struct mr_ctx {
+  mr_options opt{};
+  hipStream_t stream = nullptr;
+  bool loaded = false;
+  bool ran = false;
+  int last_model = -1;
+  int n_tr = 0, n_te = 0, n_s = 0;
+  int song_lo = 0, song_hi = 0, width = 0;
+  int block_songs = 0, n_tiles = 0;
+  int cap = 0, batch = 0;
+  DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
+  DevBuf<int> tr_songs, te_songs, trs_users, blk_ptr, nbr_v, nbr_cnt, cand_song, top_song;
+  DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
+  DevBuf<unsigned char> dense;
+  // Kernel timing ring: 4 events per timed batch (before stage 1, between
+  // stages, after stage 3), recorded without host synchronisation and
+  // resolved in flush_timing (mr_kernel_times, ring full, mr_load/destroy).
+  static constexpr int kRing = 1024;
+  std::vector<hipEvent_t> ring;
+  int ring_used = 0;
+  bool ring_has_merge[kRing] = {};
+  long long launches[3] = {0, 0, 0};
+  double ms[3] = {0, 0, 0};
+
+  void release_data() {
+    tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
+    cand_key.release(); top_key.release(); nbr_q.release();
+    tr_songs.release(); te_songs.release(); trs_users.release(); blk_ptr.release();
+    nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
+    sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
+    dense.release();
+    loaded = ran = false;
+  }
+};
+
+namespace {
+
+int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, const int32_t* col) {
+  if (!off || (off[n_rows] > 0 && !col)) return fail(MR_E_INVALID, "%s: null CSR array", what);
+  if (off[0] != 0) return fail(MR_E_INVALID, "%s: offsets[0] = %lld != 0", what, (long long)off[0]);
+  for (int r = 0; r < n_rows; ++r) {
+    if (off[r + 1] < off[r]) return fail(MR_E_INVALID, "%s: offsets decrease at row %d", what, r);
+    for (int64_t i = off[r]; i < off[r + 1]; ++i) {
+      if (col[i] < 0 || col[i] >= n_cols)
+        return fail(MR_E_INVALID, "%s: row %d has column %d outside [0,%d)", what, r, col[i], n_cols);
+      if (i > off[r] && col[i] <= col[i - 1])
+        return fail(MR_E_INVALID, "%s: row %d is not sorted strictly ascending", what, r);
+    }
+  }
+  if (off[n_rows] >= (int64_t)INT32_MAX)
+    return fail(MR_E_INVALID, "%s: %lld entries exceed the int32 index range", what, (long long)off[n_rows]);
+  return MR_OK;
+}
+
+int auto_block_songs(int width, int n_te) {
+  // Aim for >= ~1024 workgroups in stage 2, tiles of 256..16384 songs.
+  long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
+  long long bs = ((want + 255) / 256) * 256;
+  bs = std::max<long long>(256, std::min<long long>(kMaxBlockSongs, bs));
+  long long cover = ((long long)width + 255) / 256 * 256;  // no point in a tile wider than the shard
+  return (int)std::max<long long>(256, std::min(bs, cover));
+}
+
+int launch_merge(hipStream_t st, int n_users, int n_lists, int k_in, int k_out, long long user_stride,
+                 long long list_stride, const long long* keys, const int* songs, long long* out_keys,
+                 int* out_songs, double* out_scores, long long out_user0) {
+  MergeParams mp{n_lists, k_in, k_out, user_stride, list_stride, keys, songs, out_keys, out_songs,
+                 out_scores, out_user0};
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_users), dim3(kThreads), 0, st, mp);
+  MR_HIP(hipGetLastError());
+  return MR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mr_last_error(void) { return g_err.c_str(); }
+const char* mr_version(void) { return "mr_engine 0.1 (gfx950)"; }
+
+int mr_options_default(mr_options* opt) {
+  if (!opt) return fail(MR_E_INVALID, "null options");
+  std::memset(opt, 0, sizeof *opt);
+  opt->device = 0;
+  opt->frac_bits = 32;
+  opt->song_lo = 0;
+  opt->song_hi = 0;
+  opt->block_songs = 0;
+  opt->out_dtype = MR_OUT_F32;
+  opt->topk = 10;
+  opt->dense = 1;
+  opt->time_kernels = 0;
+  return MR_OK;
+}
+
+int mr_create(const mr_options* opt, mr_ctx** out) {
+  if (!out) return fail(MR_E_INVALID, "null output pointer");
+  *out = nullptr;
+  mr_options o;
+  if (opt) o = *opt; else mr_options_default(&o);
+  if (o.frac_bits < 8 || o.frac_bits > 40) return fail(MR_E_INVALID, "frac_bits %d outside [8,40]", o.frac_bits);
+  if (o.topk < 0 || o.topk > kMaxTopK) return fail(MR_E_INVALID, "topk %d outside [0,%d]", o.topk, kMaxTopK);
+  if (o.out_dtype != MR_OUT_F32 && o.out_dtype != MR_OUT_F64) return fail(MR_E_INVALID, "bad out_dtype %d", o.out_dtype);
+  if (o.block_songs < 0 || o.block_songs > kMaxBlockSongs || (o.block_songs % 256) != 0)
+    return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
+  if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
+  int ndev = 0;
+  MR_HIP(hipGetDeviceCount(&ndev));
+  if (o.device < 0 || o.device >= ndev) return fail(MR_E_INVALID, "device %d not present (%d devices)", o.device, ndev);
+  MR_HIP(hipSetDevice(o.device));
+  mr_ctx* c = new mr_ctx();
+  c->opt = o;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(MR_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  if (o.time_kernels) {
+    c->ring.resize((size_t)mr_ctx::kRing * 4);
+    for (auto& ev : c->ring) {
+      e = hipEventCreate(&ev);
+      if (e != hipSuccess) {
+        ev = nullptr;
+        mr_destroy(c);
+        return fail(MR_E_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+      }
+    }
+  }
+  *out = c;
+  return MR_OK;
+}
+
+int mr_destroy(mr_ctx* c) {
+  if (!c) return MR_OK;
+  (void)hipSetDevice(c->opt.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->release_data();
+  for (auto& ev : c->ring) if (ev) (void)hipEventDestroy(ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MR_OK;
+}
+
+void* mr_stream(const mr_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int mr_load(mr_ctx* c, const mr_dataset* d) {
+  if (!c || !d) return fail(MR_E_INVALID, "null argument");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  c->ring_used = 0;
+  c->release_data();
+  const int n_tr = d->n_train_users, n_te = d->n_test_users, n_s = d->n_songs;
+  if (n_tr < 0 || n_te <= 0 || n_s <= 0)
+    return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d n_songs=%d", n_tr, n_te, n_s);
+  if (n_tr > kMaxLdsTrainUsers)
+    return fail(MR_E_INVALID, "n_train_users=%d exceeds the LDS stage-1 limit %d of this build", n_tr,
+                kMaxLdsTrainUsers);
+  int rc;
+  if ((rc = validate_csr("train user->songs", n_tr, n_s, d->tr_off, d->tr_songs))) return rc;
+  if ((rc = validate_csr("test user->songs", n_te, n_s, d->te_off, d->te_songs))) return rc;
+  if (!d->song_count || !d->tr_len || !d->te_len) return fail(MR_E_INVALID, "null count arrays");
+  // Transpose: song -> train users (sorted, since v ascends) and count checks.
+  std::vector<int64_t> trs_off(n_s + 1, 0);
+  std::vector<int32_t> col_tr(n_s, 0), col_te(n_s, 0);
+  for (int v = 0; v < n_tr; ++v) {
+    const int64_t deg = d->tr_off[v + 1] - d->tr_off[v];
+    if (deg <= 0 || d->tr_len[v] < deg)
+      return fail(MR_E_INVALID, "train user %d: %lld distinct songs but length %d", v, (long long)deg, d->tr_len[v]);
+    for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) col_tr[d->tr_songs[i]]++;
+  }
+  for (int u = 0; u < n_te; ++u) {
+    const int64_t deg = d->te_off[u + 1] - d->te_off[u];
+    if (deg <= 0 || d->te_len[u] < deg)
+      return fail(MR_E_INVALID, "test user %d: %lld distinct songs but length %d", u, (long long)deg, d->te_len[u]);
+    for (int64_t i = d->te_off[u]; i < d->te_off[u + 1]; ++i) col_te[d->te_songs[i]]++;
+  }
+  for (int s = 0; s < n_s; ++s) {
+    if (d->song_count[s] < col_tr[s] + col_te[s] || d->song_count[s] <= 0)
+      return fail(MR_E_INVALID, "song %d: count %d below its %d distinct listeners (or zero)", s,
+                  d->song_count[s], col_tr[s] + col_te[s]);
+    trs_off[s + 1] = trs_off[s] + col_tr[s];
+  }
+  std::vector<int32_t> trs_users(std::max<int64_t>(1, trs_off[n_s]));
+  {
+    std::vector<int64_t> fill(trs_off.begin(), trs_off.end() - 1);
+    for (int v = 0; v < n_tr; ++v)
+      for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) trs_users[fill[d->tr_songs[i]]++] = v;
+  }
+  // Shard geometry.
+  const int lo = c->opt.song_lo, hi = c->opt.song_hi > 0 ? c->opt.song_hi : n_s;
+  if (lo < 0 || hi > n_s || lo >= hi) return fail(MR_E_INVALID, "song shard [%d,%d) invalid for %d songs", lo, hi, n_s);
+  const int width = hi - lo;
+  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te);
+  const int n_tiles = (width + bs - 1) / bs;
+  // Per-song / per-user fixed-point tables, computed once on the host with
+  // correctly rounded std::sqrt (java.lang.Math.sqrt semantics, MR:147/237).
+  const int F = c->opt.frac_bits;
+  const double two_f = std::ldexp(1.0, F);
+  std::vector<double> sqrt_c(n_s), sqrt_tr(std::max(1, n_tr)), sqrt_te(n_te);
+  std::vector<long long> q_song(n_s);
+  for (int s = 0; s < n_s; ++s) {
+    sqrt_c[s] = std::sqrt((double)d->song_count[s]);
+    q_song[s] = (long long)std::nearbyint(two_f / sqrt_c[s]);
+  }
+  for (int v = 0; v < n_tr; ++v) sqrt_tr[v] = std::sqrt((double)d->tr_len[v]);
+  for (int u = 0; u < n_te; ++u) sqrt_te[u] = std::sqrt((double)d->te_len[u]);
+  // Song-tiled row pointers of the train u->s CSR: blk_ptr[v][j] = first
+  // entry of S(v) with song >= min(hi, lo + j*bs).
+  std::vector<int32_t> blk_ptr((size_t)std::max(1, n_tr) * (n_tiles + 1));
+  for (int v = 0; v < n_tr; ++v) {
+    const int32_t* b = d->tr_songs + d->tr_off[v];
+    const int32_t* e = d->tr_songs + d->tr_off[v + 1];
+    for (int j = 0; j <= n_tiles; ++j) {
+      const int bound = std::min(hi, lo + j * bs);
+      blk_ptr[(size_t)v * (n_tiles + 1) + j] = (int32_t)(std::lower_bound(b, e, bound) - d->tr_songs);
+    }
+  }
+  // Test-user batch so the neighbour lists fit a device budget (8 GiB).
+  const int cap = std::max(1, n_tr);
+  const size_t per_user = (size_t)cap * 12;
+  const size_t budget = (size_t)8 << 30;
+  const int batch = (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / per_user));
+
+  hipStream_t st = c->stream;
+  if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(d->tr_off), (size_t)n_tr + 1, st))) return rc;
+  if ((rc = dev_upload(c->tr_songs, d->tr_songs, (size_t)d->tr_off[n_tr], st))) return rc;
+  if ((rc = dev_upload(c->te_off, reinterpret_cast<const long long*>(d->te_off), (size_t)n_te + 1, st))) return rc;
+  if ((rc = dev_upload(c->te_songs, d->te_songs, (size_t)d->te_off[n_te], st))) return rc;
+  if ((rc = dev_upload(c->trs_off, reinterpret_cast<const long long*>(trs_off.data()), trs_off.size(), st))) return rc;
+  if ((rc = dev_upload(c->trs_users, trs_users.data(), (size_t)trs_off[n_s], st))) return rc;
+  if ((rc = dev_upload(c->q_song, q_song.data(), q_song.size(), st))) return rc;
+  if ((rc = dev_upload(c->sqrt_c, sqrt_c.data(), sqrt_c.size(), st))) return rc;
+  if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
+  if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
+  if ((rc = dev_upload(c->blk_ptr, blk_ptr.data(), blk_ptr.size(), st))) return rc;
+  if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
+  if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
+  if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch))) return rc;
+  const int k = c->opt.topk;
+  if (k > 0) {
+    if ((rc = dev_alloc(c->cand_key, (size_t)batch * n_tiles * k))) return rc;
+    if ((rc = dev_alloc(c->cand_song, (size_t)batch * n_tiles * k))) return rc;
+    if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
+    if ((rc = dev_alloc(c->top_song, (size_t)n_te * k))) return rc;
+    if ((rc = dev_alloc(c->top_score, (size_t)n_te * k))) return rc;
+  }
+  const size_t esz = c->opt.out_dtype == MR_OUT_F64 ? 8 : 4;
+  if ((rc = dev_alloc(c->dense, c->opt.dense ? (size_t)n_te * width * esz : 1))) return rc;
+  MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
+
+  c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
+  c->song_lo = lo; c->song_hi = hi; c->width = width;
+  c->block_songs = bs; c->n_tiles = n_tiles;
+  c->cap = cap; c->batch = batch;
+  c->loaded = true;
+  c->ran = false;
+  return MR_OK;
+}
+
+int mr_shard_info(const mr_ctx* c, int32_t* lo, int32_t* hi, int32_t* n_te) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_shard_info before mr_load");
+  if (lo) *lo = c->song_lo;
+  if (hi) *hi = c->song_hi;
+  if (n_te) *n_te = c->n_te;
+  return MR_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int flush_timing(mr_ctx* c) {
+  if (c->ring_used == 0) return MR_OK;
+  MR_HIP(hipEventSynchronize(c->ring[(size_t)(c->ring_used - 1) * 4 + 3]));
+  for (int i = 0; i < c->ring_used; ++i) {
+    hipEvent_t* e = &c->ring[(size_t)i * 4];
+    float t;
+    MR_HIP(hipEventElapsedTime(&t, e[0], e[1])); c->ms[0] += t; c->launches[0]++;
+    MR_HIP(hipEventElapsedTime(&t, e[1], e[2])); c->ms[1] += t; c->launches[1]++;
+    if (c->ring_has_merge[i]) { MR_HIP(hipEventElapsedTime(&t, e[2], e[3])); c->ms[2] += t; c->launches[2]++; }
+  }
+  c->ring_used = 0;
+  return MR_OK;
+}
+
+template <int MODEL>
+int run_model(mr_ctx* c) {
+  hipStream_t st = c->stream;
+  const bool timed = c->opt.time_kernels != 0;
+  const size_t nbr_lds = (size_t)c->n_tr * 8 + kThreads * 16 + (kThreads + 1 + kWaves) * 4;
+  const size_t score_lds = (size_t)c->block_songs * 8 + (c->block_songs / 32) * 4 + kWaves * 12;
+  auto kn = k_neighbours<MODEL>;
+  MR_HIP(hipFuncSetAttribute((const void*)kn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nbr_lds));
+  void (*ks)(ScoreParams) =
+      c->opt.out_dtype == MR_OUT_F64 ? k_score<MODEL, double> : k_score<MODEL, float>;
+  MR_HIP(hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)score_lds));
+  const int k = c->opt.topk;
+  for (int user0 = 0; user0 < c->n_te; user0 += c->batch) {
+    const int nb = std::min(c->batch, c->n_te - user0);
+    NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
+                 c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
+                 c->nbr_cnt.p};
+    hipEvent_t* ev = nullptr;
+    if (timed) {
+      if (c->ring_used == mr_ctx::kRing) {
+        int rc = flush_timing(c);
+        if (rc) return rc;
+      }
+      ev = &c->ring[(size_t)c->ring_used * 4];
+      c->ring_has_merge[c->ring_used] = k > 0;
+      c->ring_used++;
+      MR_HIP(hipEventRecord(ev[0], st));
+    }
+    hipLaunchKernelGGL(kn, dim3(nb), dim3(kThreads), nbr_lds, st, np);
+    MR_HIP(hipGetLastError());
+    if (timed) MR_HIP(hipEventRecord(ev[1], st));
+    for (int y0 = 0; y0 < nb; y0 += 65535) {
+      const int ny = std::min(65535, nb - y0);
+      ScoreParams sp{user0 + y0, c->song_lo, c->song_hi, c->width, c->block_songs, c->n_tiles,
+                     c->cap, c->opt.frac_bits, k, c->opt.dense, c->te_off.p, c->te_songs.p,
+                     c->tr_songs.p, c->blk_ptr.p, c->sqrt_c.p,
+                     c->nbr_v.p + (size_t)y0 * c->cap, c->nbr_q.p + (size_t)y0 * c->cap,
+                     c->nbr_cnt.p + y0, c->dense.p,
+                     k > 0 ? c->cand_key.p + (size_t)y0 * c->n_tiles * k : nullptr,
+                     k > 0 ? c->cand_song.p + (size_t)y0 * c->n_tiles * k : nullptr};
+      hipLaunchKernelGGL(ks, dim3(c->n_tiles, ny), dim3(kThreads), score_lds, st, sp);
+      MR_HIP(hipGetLastError());
+    }
+    if (timed) MR_HIP(hipEventRecord(ev[2], st));
+    if (k > 0) {
+      int rc = launch_merge(st, nb, c->n_tiles, k, k, (long long)c->n_tiles * k, k, c->cand_key.p,
+                            c->cand_song.p, c->top_key.p, c->top_song.p, c->top_score.p, user0);
+      if (rc) return rc;
+    }
+    if (timed) MR_HIP(hipEventRecord(ev[3], st));
+  }
+  return MR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mr_run(mr_ctx* c, int model) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_run before mr_load");
+  if (model != MR_UBM && model != MR_IBM) return fail(MR_E_INVALID, "unknown model %d", model);
+  MR_HIP(hipSetDevice(c->opt.device));
+  int rc = model == MR_IBM ? run_model<MR_IBM>(c) : run_model<MR_UBM>(c);
+  if (rc) return rc;
+  c->ran = true;
+  c->last_model = model;
+  return MR_OK;
+}
+
+int mr_sync(mr_ctx* c) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+}
+
+int mr_device_outputs(const mr_ctx* c, void** dense, int32_t** ts, int64_t** tk, double** tsc) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->ran) return fail(MR_E_STATE, "no mr_run yet");
+  if (dense) *dense = c->opt.dense ? (void*)c->dense.p : nullptr;
+  if (ts) *ts = c->top_song.p;
+  if (tk) *tk = reinterpret_cast<int64_t*>(c->top_key.p);
+  if (tsc) *tsc = c->top_score.p;
+  return MR_OK;
+}
+
+int mr_copy_dense(mr_ctx* c, void* out) {
+  if (!c || !out) return fail(MR_E_INVALID, "null argument");
+  if (!c->ran) return fail(MR_E_STATE, "no mr_run yet");
+  if (!c->opt.dense) return fail(MR_E_STATE, "context created with dense=0");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const size_t esz = c->opt.out_dtype == MR_OUT_F64 ? 8 : 4;
+  MR_HIP(hipMemcpyAsync(out, c->dense.p, (size_t)c->n_te * c->width * esz, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+}
+
+int mr_copy_topk(mr_ctx* c, int32_t* songs, double* scores, int64_t* keys) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->ran) return fail(MR_E_STATE, "no mr_run yet");
+  if (c->opt.topk <= 0) return fail(MR_E_STATE, "context created with topk=0");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const size_t n = (size_t)c->n_te * c->opt.topk;
+  if (songs) MR_HIP(hipMemcpyAsync(songs, c->top_song.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  if (scores) MR_HIP(hipMemcpyAsync(scores, c->top_score.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+  if (keys) MR_HIP(hipMemcpyAsync(keys, c->top_key.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+}
+
+int mr_copy_topk_device(mr_ctx* c, int32_t* songs, int64_t* keys) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->ran) return fail(MR_E_STATE, "no mr_run yet");
+  if (c->opt.topk <= 0) return fail(MR_E_STATE, "context created with topk=0");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const size_t n = (size_t)c->n_te * c->opt.topk;
+  if (songs) MR_HIP(hipMemcpyAsync(songs, c->top_song.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (keys) MR_HIP(hipMemcpyAsync(keys, c->top_key.p, n * 8, hipMemcpyDeviceToDevice, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+}
+
+int mr_score_dense(mr_ctx* c, int model, void* out) {
+  int rc = mr_run(c, model);
+  if (rc) return rc;
+  return mr_copy_dense(c, out);
+}
+
+int mr_topk(mr_ctx* c, int model, int k, int32_t* songs, double* scores, int64_t* keys) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (k != c->opt.topk) return fail(MR_E_INVALID, "k=%d differs from the context's topk=%d", k, c->opt.topk);
+  int rc = mr_run(c, model);
+  if (rc) return rc;
+  return mr_copy_topk(c, songs, scores, keys);
+}
+
+int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                         const int64_t* keys_in, const double* /*scores_in*/, int32_t* songs_out,
+                         int64_t* keys_out, double* scores_out) {
+  if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
+  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
+  MR_HIP(hipSetDevice(c->opt.device));
+  int rc = launch_merge(c->stream, n_te, n_shards, k, k, k, (long long)n_te * k,
+                        reinterpret_cast<const long long*>(keys_in), songs_in,
+                        reinterpret_cast<long long*>(keys_out), songs_out, scores_out, 0);
+  if (rc) return rc;
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+}
+
+int mr_kernel_times(mr_ctx* c, int32_t which, int64_t* launches, double* total_ms, int32_t reset) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (which < 0 || which > 2) return fail(MR_E_INVALID, "kernel index %d outside [0,2]", which);
+  MR_HIP(hipSetDevice(c->opt.device));
+  int rc = flush_timing(c);
+  if (rc) return rc;
+  if (launches) *launches = c->launches[which];
+  if (total_ms) *total_ms = c->ms[which];
+  if (reset) { c->launches[which] = 0; c->ms[which] = 0.0; }
+  return MR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,152 @@
+"""Python handle on one engine context (one GPU, one song-range shard).
+
+Thin wrapper over the C ABI (include/mr_engine.h); all compute runs in the HIP
+kernels of csrc/mr_engine.hip. There is no CPU fallback: without a GPU or
+without the built library every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple, Union
+
+import numpy as np
+
+from . import _lib
+from .dataset import Dataset
+
+MODELS = {"ubm": _lib.MR_UBM, "ibm": _lib.MR_IBM, _lib.MR_UBM: _lib.MR_UBM, _lib.MR_IBM: _lib.MR_IBM}
+KERNELS = {"neighbours": 0, "score": 1, "merge": 2}
+
+
+def model_id(model: Union[str, int]) -> int:
+    try:
+        return MODELS[model]
+    except KeyError:
+        raise ValueError(f"unknown model {model!r}: use 'ubm' or 'ibm'") from None
+
+
+class Engine:
+    def __init__(self, dataset: Dataset, *, device: int = 0, frac_bits: int = 32, song_lo: int = 0,
+                 song_hi: int = 0, block_songs: int = 0, out_dtype: str = "f32", topk: int = 10,
+                 dense: bool = True, time_kernels: bool = False):
+        self._L = _lib.lib()
+        opt = _lib.MrOptions()
+        _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
+        opt.device = device
+        opt.frac_bits = frac_bits
+        opt.song_lo = song_lo
+        opt.song_hi = song_hi
+        opt.block_songs = block_songs
+        opt.out_dtype = {"f32": _lib.MR_OUT_F32, "f64": _lib.MR_OUT_F64}[out_dtype]
+        opt.topk = topk
+        opt.dense = 1 if dense else 0
+        opt.time_kernels = 1 if time_kernels else 0
+        self.opt = opt
+        self.dtype = np.float32 if out_dtype == "f32" else np.float64
+        self._h = ctypes.c_void_p()
+        _lib.check(self._L.mr_create(ctypes.byref(opt), ctypes.byref(self._h)), "mr_create")
+        self.dataset = dataset
+        try:
+            cd = dataset.c_struct()
+            _lib.check(self._L.mr_load(self._h, ctypes.byref(cd)), "mr_load")
+        except Exception:
+            self.close()
+            raise
+        lo, hi, nte = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self._L.mr_shard_info(self._h, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(nte)),
+                   "mr_shard_info")
+        self.song_lo, self.song_hi, self.n_test = lo.value, hi.value, nte.value
+        self.width = self.song_hi - self.song_lo
+        self.topk_k = topk
+
+    # ---- lifecycle ----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.mr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- compute --------------------------------------------------------------
+    def run(self, model: Union[str, int]) -> None:
+        """Asynchronous: score every pair of the shard into device buffers."""
+        _lib.check(self._L.mr_run(self._h, model_id(model)), "mr_run")
+
+    def sync(self) -> None:
+        _lib.check(self._L.mr_sync(self._h), "mr_sync")
+
+    @property
+    def stream(self) -> int:
+        return self._L.mr_stream(self._h) or 0
+
+    def dense(self) -> np.ndarray:
+        """n_test x width scores of the last run (NaN = heard song, no pair)."""
+        out = np.empty((self.n_test, self.width), dtype=self.dtype)
+        _lib.check(self._L.mr_copy_dense(self._h, out.ctypes.data_as(ctypes.c_void_p)), "mr_copy_dense")
+        return out
+
+    def topk(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(songs int32, scores f64, keys int64), each n_test x k, of the last run."""
+        k = self.topk_k
+        songs = np.empty((self.n_test, k), dtype=np.int32)
+        scores = np.empty((self.n_test, k), dtype=np.float64)
+        keys = np.empty((self.n_test, k), dtype=np.int64)
+        _lib.check(self._L.mr_copy_topk(self._h, songs.ctypes.data_as(ctypes.c_void_p),
+                                        scores.ctypes.data_as(ctypes.c_void_p),
+                                        keys.ctypes.data_as(ctypes.c_void_p)), "mr_copy_topk")
+        return songs, scores, keys
+
+    def copy_topk_device(self, songs_ptr: int, keys_ptr: int) -> None:
+        """Copy the last run's top-k lists into device buffers (D2D, synchronous)."""
+        _lib.check(self._L.mr_copy_topk_device(self._h, songs_ptr, keys_ptr), "mr_copy_topk_device")
+
+    def score_dense(self, model: Union[str, int]) -> np.ndarray:
+        self.run(model)
+        return self.dense()
+
+    def device_outputs(self) -> Tuple[int, int, int, int]:
+        ptrs = [ctypes.c_void_p() for _ in range(4)]
+        _lib.check(self._L.mr_device_outputs(self._h, *[ctypes.byref(p) for p in ptrs]), "mr_device_outputs")
+        return tuple(p.value or 0 for p in ptrs)
+
+    def merge_topk_device(self, n_shards: int, songs_ptr: int, keys_ptr: int, out_songs_ptr: int,
+                          out_keys_ptr: int, out_scores_ptr: int = 0) -> None:
+        """Merge n_shards gathered [shard][n_test][k] device lists on this GPU."""
+        _lib.check(self._L.mr_topk_merge_device(self._h, n_shards, self.n_test, self.topk_k, songs_ptr, keys_ptr,
+                                                None, out_songs_ptr, out_keys_ptr, out_scores_ptr or None),
+                   "mr_topk_merge_device")
+
+    def kernel_times(self, kernel: Union[str, int], reset: bool = False) -> Tuple[int, float]:
+        n = ctypes.c_int64()
+        ms = ctypes.c_double()
+        which = KERNELS[kernel] if isinstance(kernel, str) else kernel
+        _lib.check(self._L.mr_kernel_times(self._h, which, ctypes.byref(n), ctypes.byref(ms), 1 if reset else 0),
+                   "mr_kernel_times")
+        return n.value, ms.value
+
+
+def merge_topk_host(songs: np.ndarray, keys: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Merge [n_shards][n_test][k] per-shard lists (song ids global) -> n_test x k
+    by (key desc, song asc): the exchange step of a song-sharded run, host side."""
+    L = _lib.lib()
+    songs = np.ascontiguousarray(songs, dtype=np.int32)
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    g, n_te, k = songs.shape
+    os_ = np.empty((n_te, k), dtype=np.int32)
+    ok = np.empty((n_te, k), dtype=np.int64)
+    osc = np.empty((n_te, k), dtype=np.float64)
+    _lib.check(L.mr_topk_merge_host(g, n_te, k, songs.ctypes.data_as(ctypes.c_void_p),
+                                    keys.ctypes.data_as(ctypes.c_void_p), None,
+                                    os_.ctypes.data_as(ctypes.c_void_p), ok.ctypes.data_as(ctypes.c_void_p),
+                                    osc.ctypes.data_as(ctypes.c_void_p)), "mr_topk_merge_host")
+    return os_, osc, ok

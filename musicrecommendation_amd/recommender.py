@@ -1,0 +1,121 @@
+"""Host-side mirror of the reference class ``MusicRecommender``
+(src/main/scala/music_recommandation/MusicRecommender.scala, MR:12).
+
+Same constructor inputs (train, test and test-labels triplet sources, MR:12),
+same public method names and result shape — ``Array[(user, (song, score))]``
+for every (test user, unheard song) pair — so a caller of the reference can
+switch over. The scoring runs on the MI355X engine (one batched call per
+model instead of one closure call per pair, MR:105-125); the ingest runs in
+the native C++ TSV reader (MR:26-91).
+
+Emission order: the reference emits s-major, u-minor in JVM HashSet order
+(MR:105-111), which no other runtime reproduces; we emit s-major, u-minor in
+lexicographic id order. The driver sorts both by (user, song, -score)
+anyway (main.scala:57-59); ``sorted_model`` gives that order directly.
+The ``*P`` variants exist for API parity; on the GPU both are the parallel path.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+from typing import Iterable, List, Optional, Tuple, Union
+
+import numpy as np
+
+from .dataset import Dataset
+from .engine import Engine
+from . import evaluation
+
+Model = List[Tuple[str, Tuple[str, float]]]
+Source = Union[str, os.PathLike, Iterable[str]]
+
+
+def _as_path(src: Source, tmpdir: str, name: str) -> str:
+    if isinstance(src, (str, os.PathLike)) and os.path.exists(src):
+        return os.fspath(src)
+    path = os.path.join(tmpdir, name)
+    with open(path, "w") as f:
+        for line in src:  # a BufferedSource-like iterable of lines
+            f.write(line if line.endswith("\n") else line + "\n")
+    return path
+
+
+class MusicRecommender:
+    def __init__(self, trainFile: Source, testFile: Source, testLabelsFile: Source, *, device: int = 0,
+                 out_dtype: str = "f64", topk: int = 10):
+        with tempfile.TemporaryDirectory() as td:
+            self.dataset = Dataset.from_tsv(_as_path(trainFile, td, "train.txt"),
+                                            _as_path(testFile, td, "test.txt"),
+                                            _as_path(testLabelsFile, td, "labels.txt"))
+        self._device = device
+        self._out_dtype = out_dtype
+        self._topk = topk
+        self._engine: Optional[Engine] = None
+
+    # ---- engine ------------------------------------------------------------
+    def engine(self) -> Engine:
+        if self._engine is None:
+            self._engine = Engine(self.dataset, device=self._device, out_dtype=self._out_dtype, topk=self._topk)
+        return self._engine
+
+    def scores(self, model: str) -> np.ndarray:
+        """Dense n_test x n_songs scores (NaN for heard songs)."""
+        return self.engine().score_dense(model)
+
+    def recommendations(self, model: str) -> Tuple[np.ndarray, np.ndarray]:
+        """Per test user, the top-k (song ids, scores) by (score desc, song asc)."""
+        e = self.engine()
+        e.run(model)
+        songs, scores, _keys = e.topk()
+        return songs, scores
+
+    def _to_model(self, dense: np.ndarray) -> Model:
+        ds = self.dataset
+        sn, un = ds.song_names, ds.test_names
+        out: Model = []
+        users = [un(u) for u in range(ds.n_test)]
+        for s in range(ds.n_songs):  # s-major, u-minor (MR:106-108)
+            col = dense[:, s]
+            name = sn(s)
+            for u in range(ds.n_test):
+                x = col[u]
+                if not np.isnan(x):  # heard songs emit no pair (MR:109)
+                    out.append((users[u], (name, float(x))))
+        return out
+
+    # ---- reference API (MR:132-307) -------------------------------------------
+    def getUserBasedModel(self) -> Model:
+        return self._to_model(self.scores("ubm"))
+
+    def getUserBasedModelP(self) -> Model:
+        return self.getUserBasedModel()
+
+    def getItemBasedModel(self) -> Model:
+        return self._to_model(self.scores("ibm"))
+
+    def getItemBasedModelP(self) -> Model:
+        return self.getItemBasedModel()
+
+    @staticmethod
+    def sorted_model(model: Model) -> Model:
+        """main.scala:57-59 ordering: (user, song, -score)."""
+        return sorted(model, key=lambda t: (t[0], t[1][0], -t[1][1]))
+
+    # ---- evaluation (MR:636-639) ------------------------------------------------
+    def evaluateModel(self, model: Union[Model, np.ndarray], parallel: bool = False) -> float:
+        dense = model if isinstance(model, np.ndarray) else self._from_model(model)
+        return evaluation.threshold_map(dense, self.dataset)
+
+    def _from_model(self, model: Model) -> np.ndarray:
+        ds = self.dataset
+        sidx = {ds.song_names(i): i for i in range(ds.n_songs)}
+        uidx = {ds.test_names(i): i for i in range(ds.n_test)}
+        dense = np.full((ds.n_test, ds.n_songs), np.nan)
+        for u, (s, x) in model:
+            dense[uidx[u], sidx[s]] = x
+        return dense
+
+    def close(self) -> None:
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None

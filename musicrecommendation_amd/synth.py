@@ -1,0 +1,140 @@
+"""Seeded synthetic Taste-Profile-shaped triplets.
+
+The real subsets (train_N_M.txt ...) are git-ignored in the reference and the
+48M-row Echo Nest Taste Profile is not in this image, so every config runs on
+synthetic data built to the split rule of the reference's data-prep notebook
+(dataExtraction.ipynb):
+  * song popularity Zipf(alpha) over 384,546 song ids (NB:126), randomly
+    permuted onto ids;
+  * history length max(10, round(lognormal(3.51, 0.86))) per user (fitted to
+    NB cell 10: min 10, median 29, mean 53.2);
+  * each user draws distinct songs; playcount 1 (ignored, MR:35);
+  * train = first n_train users, test = next n_test (NB:149, NB:301);
+  * each test user: first ceil(n/2) rows visible, the rest are labels (NB:571-573).
+``alpha=None`` bisects alpha so that the number of distinct songs lands within
+±5 % of ``target_songs`` (the README's song count for the named config).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from .dataset import Dataset
+
+N_SONG_UNIVERSE = 384_546  # distinct songs in the Taste Profile (NB:126)
+
+# Named configs of BASELINE.json (n_train, n_test, seed, target distinct songs).
+CONFIGS = {
+    "c1": (100, 10, 1, 4798),      # README.md:72 (train_100_10)
+    "c2": (500, 10, 2, 16785),     # README.md:96 (train_500_10)
+    "c3": (10_000, 1_000, 3, None),
+    "tiny": (20, 5, 7, None),
+    "small": (60, 8, 11, None),
+}
+# alpha found by calibrate_alpha for the configs with a song-count target
+# (cached so every run uses the same value; re-derive with calibrate_alpha).
+ALPHA = {"c1": 0.7, "c2": 0.8625}
+
+
+@dataclass
+class Triplets:
+    train_u: np.ndarray
+    train_s: np.ndarray
+    test_u: np.ndarray
+    test_s: np.ndarray
+    label_u: np.ndarray
+    label_s: np.ndarray
+    alpha: float
+
+    def dataset(self) -> Dataset:
+        return Dataset.from_triplets(self.train_u, self.train_s, self.test_u, self.test_s,
+                                     self.label_u, self.label_s)
+
+    def n_songs(self) -> int:
+        return int(np.unique(np.concatenate([self.train_s, self.test_s])).size)
+
+
+def _user_songs(rng: np.random.Generator, cdf: np.ndarray, perm: np.ndarray) -> np.ndarray:
+    """One user's history: length max(10, round(lognormal(3.51, 0.86))), distinct
+    songs drawn by popularity (oversample with replacement, keep first draws)."""
+    n_universe = cdf.size
+    n = int(min(n_universe, max(10, round(float(rng.lognormal(3.51, 0.86))))))
+    have = np.zeros(0, dtype=np.int64)
+    for _ in range(64):
+        ranks = np.searchsorted(cdf, rng.random(2 * n + 8), side="right")
+        cat = np.concatenate([have, perm[np.minimum(ranks, n_universe - 1)]])
+        _, first = np.unique(cat, return_index=True)
+        first.sort()
+        have = cat[first][:n]
+        if have.size == n:
+            return have
+    raise RuntimeError("synthetic draw did not converge")
+
+
+def _popularity(seed: int, alpha: float, n_universe: int):
+    perm = np.random.default_rng([seed, 0]).permutation(n_universe).astype(np.int64)
+    w = np.arange(1, n_universe + 1, dtype=np.float64) ** (-alpha)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return cdf, perm
+
+
+def generate(n_train: int, n_test: int, seed: int, alpha: Optional[float] = None,
+             target_songs: Optional[int] = None, n_universe: int = N_SONG_UNIVERSE,
+             test_offset: int = 0) -> Triplets:
+    """Train user i draws from stream (seed, 1, i), test user j from (seed, 2, j):
+    datasets are prefix-consistent in n_train and n_test (the first 10 test
+    users of a 500/40 dataset are those of 500/10)."""
+    if alpha is None and target_songs is not None:
+        alpha = calibrate_alpha(n_train, n_test, seed, target_songs, n_universe)
+    if alpha is None:
+        alpha = 0.87
+    cdf, perm = _popularity(seed, alpha, n_universe)
+    tr_u, tr_s = [], []
+    for i in range(n_train):
+        songs = _user_songs(np.random.default_rng([seed, 1, i]), cdf, perm)
+        tr_u.append(np.full(songs.size, i, dtype=np.int64))
+        tr_s.append(songs)
+    te_u, te_s, lb_u, lb_s = [], [], [], []
+    for j in range(test_offset, test_offset + n_test):
+        songs = _user_songs(np.random.default_rng([seed, 2, j]), cdf, perm)
+        key = n_train + j  # user keys: train 0..n_train-1, then test users
+        vis = math.ceil(songs.size / 2)  # NB:571-573
+        te_u.append(np.full(vis, key, dtype=np.int64)); te_s.append(songs[:vis])
+        lb_u.append(np.full(songs.size - vis, key, dtype=np.int64)); lb_s.append(songs[vis:])
+    cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64)  # noqa: E731
+    return Triplets(cat(tr_u), cat(tr_s), cat(te_u), cat(te_s), cat(lb_u), cat(lb_s), float(alpha))
+
+
+def calibrate_alpha(n_train: int, n_test: int, seed: int, target_songs: int,
+                    n_universe: int = N_SONG_UNIVERSE, tol: float = 0.05) -> float:
+    """Bisect alpha (distinct songs decrease with alpha) to within ±tol of target."""
+    lo, hi = 0.0, 1.6
+    best = None
+    for _ in range(30):
+        mid = 0.5 * (lo + hi)
+        t = generate(n_train, n_test, seed, alpha=mid, n_universe=n_universe)
+        ns = t.n_songs()
+        err = abs(ns - target_songs) / target_songs
+        if best is None or err < best[0]:
+            best = (err, mid)
+        if err <= tol * 0.2:
+            break
+        if ns > target_songs:
+            lo = mid
+        else:
+            hi = mid
+    return round(best[1], 6)
+
+
+def config(name: str, n_test: Optional[int] = None) -> Triplets:
+    """Named config; n_test overrides the test-user count (weak-scaling runs
+    use n_test = 10 x GPUs with the same train set and the same alpha)."""
+    n_tr, n_te, seed, target = CONFIGS[name]
+    alpha = ALPHA.get(name)
+    if alpha is None and target is not None:
+        alpha = calibrate_alpha(n_tr, n_te, seed, target)
+    return generate(n_tr, n_test if n_test is not None else n_te, seed, alpha=alpha)

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace stats.
+# Each GPU step has its own time limit; a crash/abort/timeout ends the session
+# (test assertion failures, exit 1, do not).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+STEPS=${STEPS:-tests,smoke,bench,prof}
+
+run() {  # name limit cmd...
+  local name=$1 limit=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc in $name: stopping" | tee -a "$OUT/session.log"; exit $rc; fi
+  return $rc
+}
+
+rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/gpu.txt" || true
+case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;; esac
+case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
+case ",$STEPS," in *,bench,*) run bench 600 python bench.py ;; esac
+case ",$STEPS," in *,prof,*)
+  export TMPDIR=/tmp
+  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 200 ;;
+esac
+exit 0
