@@ -64,6 +64,15 @@ def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
     return {"neighbours": b1, "score": b2, "merge": 12 * k * ds.n_test}
 
 
+def kernel_bytes(ab, fused: bool):
+    """Per-launch algorithmic bytes of the launched kernels: the fused shape
+    runs all three stages in k_score; the separate shape runs stage 1 in
+    k_neighbours and stages 2+3 in k_score."""
+    if fused:
+        return {"score": ab["neighbours"] + ab["score"] + ab["merge"]}
+    return {"neighbours": ab["neighbours"], "score": ab["score"] + ab["merge"]}
+
+
 def cpu_baseline(ds, model: str, seconds: float):
     """Literal restatement of getItemBasedModelP (oracle/literal.c, string ids,
     linear contains, pthreads over songs x users like MR:119-125) timed on a
@@ -142,7 +151,7 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     drain()
-    for kname in ("neighbours", "score", "merge"):
+    for kname in ("neighbours", "score"):
         eng.kernel_times(kname, reset=True)
 
     if world > 1:
@@ -157,7 +166,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    kt = {k: eng.kernel_times(k) for k in ("neighbours", "score", "merge")}
+    kt = {k: eng.kernel_times(k) for k in ("neighbours", "score")}
     stats = torch.tensor([elapsed, float(pairs_rank)], dtype=torch.float64, device="cuda")
     if world > 1:
         t_max = stats[:1].clone()
@@ -170,11 +179,12 @@ def main() -> None:
 
     if rank == 0:
         value = pairs_all * args.steps / elapsed_max
-        ab = algorithmic_bytes(ds, 4, 10)
+        ab_stage = algorithmic_bytes(ds, 4, 10)
+        ab = kernel_bytes(ab_stage, eng.fused)
         avg_us = {k: (kt[k][1] / kt[k][0] * 1e3 if kt[k][0] else None) for k in kt}
-        dom = max(("neighbours", "score", "merge"), key=lambda k: avg_us[k] or 0.0)
+        dom = max(ab, key=lambda k: avg_us[k] or 0.0)
         achieved = ab[dom] / (avg_us[dom] * 1e-6) / 1e9
-        step_bytes = sum(ab.values())
+        step_bytes = sum(ab_stage.values())
         traffic = args.traffic_bytes
         # quality companions on the last step's outputs (host-side, untimed)
         from musicrecommendation_amd import evaluation
@@ -210,7 +220,8 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"k_score ({dom})" if dom == "score" else dom,
+                "kernel": ("k_score (fused: stages 1+2+3)" if eng.fused else "k_score (stages 2+3)")
+                if dom == "score" else "k_neighbours (stage 1)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -220,6 +231,7 @@ def main() -> None:
                 "avg_launch_us": avg_us[dom],
             },
             "kernels_avg_us": avg_us,
+            "launch": {"fused": eng.fused, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles},
             "step_algorithmic_bytes": step_bytes,
             "step_GBps": step_bytes / (elapsed_max / args.steps) / 1e9,
             "mAP@10": map10,

@@ -105,7 +105,9 @@ typedef struct mr_options {
   int32_t topk;        /* k of the per-test-user recommendation list (0 = off, <= 64; default 10) */
   int32_t dense;       /* 1 (default) = write the dense model; 0 = top-k only */
   int32_t time_kernels;/* 1 = record HIP events around each kernel in mr_run (see mr_kernel_times) */
-  int32_t reserved[7];
+  int32_t stage1;      /* launch shape: 0 = auto, 1 = fused (one kernel; stage 1 recomputed per
+                          song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel */
+  int32_t reserved[6];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;
@@ -123,6 +125,10 @@ int mr_load(mr_ctx* ctx, const mr_dataset* d);
 /* Shard geometry after mr_load: [*song_lo, *song_hi) and the number of
  * test users. The dense model of this context is n_te x (song_hi - song_lo). */
 int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
+
+/* Launch shape chosen by mr_load: fused (1) or separate stage 1 (0), songs
+ * per LDS tile and tiles per test user. */
+int mr_launch_info(const mr_ctx* ctx, int32_t* fused, int32_t* block_songs, int32_t* n_tiles);
 
 /*
  * Score every (test user, song) pair of the shard for `model`, leaving the
@@ -168,8 +174,9 @@ int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
                          int32_t* songs_out, int64_t* keys_out, double* scores_out);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
- * (0 = neighbour weights, 1 = song-tile scoring, 2 = top-k merge) the number
- * of timed launches and their summed device milliseconds; reset=1 clears. */
+ * (0 = separate stage-1 neighbour kernel, 1 = the scoring kernel — stage 2,
+ * fused stage 1 and the in-launch top-k merge —, 2 = reserved) the number of
+ * timed launches and their summed device milliseconds; reset=1 clears. */
 int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
 
 /* HIP stream of the context (as void* = hipStream_t). */

@@ -66,7 +66,8 @@ class MrOptions(ctypes.Structure):
         ("topk", c_int32),
         ("dense", c_int32),
         ("time_kernels", c_int32),
-        ("reserved", c_int32 * 7),
+        ("stage1", c_int32),
+        ("reserved", c_int32 * 6),
     ]
 
 
@@ -83,6 +84,7 @@ SIGNATURES = {
     "mr_destroy": (c_int, [c_void_p]),
     "mr_load": (c_int, [c_void_p, POINTER(MrDataset)]),
     "mr_shard_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "mr_launch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),
     "mr_device_outputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),

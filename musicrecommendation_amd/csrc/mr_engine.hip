@@ -6,17 +6,23 @@
 //   UBM cosine + rank         MR:140-166
 //   IBM cosine + rank         MR:230-257
 // by a two-stage sparse computation (SURVEY.md §0.1 "two-hop identity"):
-//   stage 1 (k_neighbours): per test user u, one weight per train neighbour v
+//   stage 1, per test user u, one weight per train neighbour v
 //       ibm: y_v = Σ_{s2 ∈ T(u) ∩ S(v)} q(s2),   q(s2) = rint(2^F / sqrt c(s2))
 //       ubm: o_v = |T(u) ∩ S(v)|,  q_v = rint(2^F · o_v / (sqrt|T(u)| · sqrt|S(v)|))
-//   stage 2 (k_score): per (u, song tile) an LDS int64 accumulator
+//   stage 2, per (u, song tile) an LDS int64 accumulator
 //       acc[s] = Σ_{v ∈ N(u), s ∈ S(v)} weight_v
 //       ibm: score = acc·2^-F / sqrt c(s);  ubm: score = acc·2^-F
-//     + dense write (NaN for heard songs, MR:109) + the tile's top-k candidates
-//   stage 3 (k_topk_merge): per test user, top-k over the tile candidates.
+//     + dense write (NaN for heard songs, MR:109) + the tile's top-k
+//   stage 3, per test user, the top-k over all tiles, done inside the same
+//       launch by the workgroup that finishes the user's last tile.
+// Two launch shapes:
+//   fused    (small train sets): ONE kernel; every (u, tile) workgroup
+//            rebuilds u's neighbour weights in LDS (k_score<.., FUSED=true>);
+//   separate (large train sets): k_neighbours writes compacted neighbour
+//            lists, then k_score<.., FUSED=false> reads them.
 // Integer accumulation is associative, so every launch geometry, shard count
 // and the CPU fixed-point oracle (oracle/fixedpoint.c) give bit-identical
-// scores and hence identical top-k order. Build with -ffp-contract=off.
+// scores and hence identical top-k order. Built with -ffp-contract=off.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,12 +39,14 @@
 
 namespace {
 
-constexpr int kThreads = 256;            // 4 waves of 64
+constexpr int kThreads = 256;             // 4 waves of 64
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxTopK = 64;
-constexpr int kMaxBlockSongs = 16384;    // 128 KiB of int64 accumulators (LDS is 160 KiB)
-constexpr int kMaxLdsTrainUsers = 16384; // stage-1 dense neighbour array in LDS (int64)
-constexpr long long kKeyNone = -1;       // valid keys are bit patterns of doubles >= 0
+constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS is 160 KiB)
+constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64)
+constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live together
+constexpr int kMergeStage = 2048;         // candidates staged in LDS per merge pass
+constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
 
 thread_local std::string g_err = "no error";
 
@@ -78,6 +86,39 @@ namespace {
   } while (0)
 
 // ---------------------------------------------------------------------------
+// LDS layout of k_score (bytes; every region 16-byte aligned). Region A holds
+// the tile accumulators (+ the fused path's neighbour array Y) and is reused
+// as the merge staging area once the tile's own top-k has been published.
+// ---------------------------------------------------------------------------
+struct ScoreLds {
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, total;
+};
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int merge_cap) {
+  ScoreLds L;
+  const int a = bs * 8 + fused_ntr * 8;
+  const int m = merge_cap * 12;
+  L.acc = 0;
+  L.y = bs * 8;
+  int o = align16(a > m ? a : m);
+  L.heard = o; o = align16(o + (bs / 32) * 4);
+  const int fused = fused_ntr > 0 ? 1 : 0;
+  L.s_lo = o; o += fused * kThreads * 8;
+  L.s_w = o; o += fused * kThreads * 8;
+  L.s_pre = o; o = align16(o + (kThreads + 1) * 4);
+  L.s_scan = o; o = align16(o + kWaves * 4);
+  L.wk = o; o = align16(o + kWaves * kMaxTopK * 8);
+  L.ws = o; o = align16(o + kWaves * kMaxTopK * 4);
+  L.fk = o; o = align16(o + kMaxTopK * 8);
+  L.fs = o; o = align16(o + kMaxTopK * 4);
+  L.flag = o; o = align16(o + 4);
+  L.total = o;
+  return L;
+}
+
+// ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
 
@@ -109,54 +150,86 @@ __device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, 
   return ka > kb || (ka == kb && sa < sb);
 }
 
-// Block-wide best candidate; every thread returns the same (key, song).
-__device__ __forceinline__ void block_best(long long& k, int& s, long long* sk, int* ss) {
+// Wave-wide best candidate (all 64 lanes return it); shuffles only, no LDS.
+__device__ __forceinline__ void wave_best(long long& k, int& s) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
-    long long ko = __shfl_xor(k, m, 64);
-    int so = __shfl_xor(s, m, 64);
+    const long long ko = __shfl_xor(k, m, 64);
+    const int so = __shfl_xor(s, m, 64);
     if (cand_before(ko, so, k, s)) { k = ko; s = so; }
   }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { sk[w] = k; ss[w] = s; }
-  __syncthreads();
-  k = sk[0]; s = ss[0];
-#pragma unroll
-  for (int i = 1; i < kWaves; ++i)
-    if (cand_before(sk[i], ss[i], k, s)) { k = sk[i]; s = ss[i]; }
-  __syncthreads();
 }
 
-// Top-k selection by repeated block argmax: round r picks the best candidate
-// strictly after round r-1's winner in the total order (candidates are
-// distinct songs, so no "taken" marks are needed). Load(i) -> (key, song);
-// key < 0 means "not a candidate".
-template <typename Load>
-__device__ __forceinline__ void block_select_topk(int n, int k, Load load, long long* out_key,
-                                                  int* out_song, long long* sk, int* ss) {
+// One wave selects its top-k: round r takes the best candidate strictly after
+// round r-1's winner in the total order (candidates are distinct songs, so no
+// "taken" marks). Lane l supplies m_l candidates via get(j, key, song); key < 0
+// = no candidate. Lane 0 writes out_k/out_s[0..k); missing slots -> (-1, -1).
+template <typename Get>
+__device__ __forceinline__ void wave_topk(int m, Get get, int k, long long* out_k, int* out_s) {
+  const int lane = threadIdx.x & 63;
   long long pk = LLONG_MAX;
   int ps = -1;
   int r = 0;
   for (; r < k; ++r) {
     long long bk = kKeyNone;
     int bs = INT_MAX;
-    for (int i = threadIdx.x; i < n; i += kThreads) {
+    for (int j = 0; j < m; ++j) {
       long long ck;
       int cs;
-      load(i, ck, cs);
+      get(j, ck, cs);
       if (ck >= 0 && cand_before(pk, ps, ck, cs) && cand_before(ck, cs, bk, bs)) { bk = ck; bs = cs; }
     }
-    block_best(bk, bs, sk, ss);
+    wave_best(bk, bs);  // wave-uniform from here
     if (bk < 0) break;
-    if (threadIdx.x == 0) { out_key[r] = bk; out_song[r] = bs; }
-    pk = bk; ps = bs;
+    if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
+    pk = bk;
+    ps = bs;
   }
-  for (int i = r + threadIdx.x; i < k; i += kThreads) { out_key[i] = kKeyNone; out_song[i] = -1; }
+  for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
+}
+
+// Block top-k over elements [0, n): wave w scans elements w*64+lane (+256 j),
+// then wave 0 selects from the 4 wave lists. Two barriers in total.
+template <typename Get>
+__device__ __forceinline__ void block_topk(int n, Get get, int k, long long* wk, int* ws, long long* out_k,
+                                           int* out_s) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int first = w * 64 + lane;
+  const int m = first < n ? (n - first + kThreads - 1) / kThreads : 0;
+  wave_topk(
+      m, [&](int j, long long& key, int& song) { get(first + j * kThreads, key, song); }, k, wk + w * k,
+      ws + w * k);
+  __syncthreads();
+  if (w == 0) {
+    const int tot = kWaves * k;
+    const int m0 = lane < tot ? (tot - lane + 63) / 64 : 0;
+    wave_topk(
+        m0,
+        [&](int j, long long& key, int& song) {
+          key = wk[lane + j * 64];
+          song = ws[lane + j * 64];
+        },
+        k, out_k, out_s);
+  }
+  __syncthreads();
+}
+
+// sc1 (L2-coherent, agent-scope) stores/loads for the in-launch hand-off of
+// tile candidates to the user's last workgroup (MI355X_MICROARCH.md, "Valid
+// forms", row 1: sc1 stores, vmcnt(0), barrier, one agent atomic add per
+// workgroup; the last adder loads with sc1 loads).
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
-// stage 1: neighbour weights (one workgroup per test user, dense LDS array
-// over the train users). MR:140-149 (ubm numerator) / MR:230-239 (ibm).
+// stage 1, separate shape: one workgroup per test user, dense LDS array over
+// the train users, compacted (v, weight) lists to global. MR:140-149 / MR:230-239.
 // ---------------------------------------------------------------------------
 struct NbrParams {
   int n_tr;
@@ -175,51 +248,72 @@ struct NbrParams {
   int* nbr_cnt;              // [batch]
 };
 
+// Accumulate Y[v] += w(s2) over v ∈ L_tr(s2), s2 ∈ T(u): a flattened walk over
+// the listener lists of T(u), 256 songs of T(u) at a time. If `heard` is
+// non-null, also mark T(u) ∩ [blo, bhi) in the tile's heard bitmap.
 template <int MODEL>
-__global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
-  extern __shared__ unsigned long long smem[];
-  unsigned long long* Y = smem;                         // [n_tr]
-  long long* s_lo = reinterpret_cast<long long*>(Y + p.n_tr);  // [256] list start
-  long long* s_w = s_lo + kThreads;                     // [256] weight
-  int* s_pre = reinterpret_cast<int*>(s_w + kThreads);  // [257] exclusive prefix
-  int* s_scan = s_pre + kThreads + 1;                   // [kWaves]
-
-  const int bu = blockIdx.x;           // user within batch
-  const int u = p.user0 + bu;
+__device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, long long t0, long long t1,
+                                                      const int* te_songs, const long long* trs_off,
+                                                      const int* trs_users, const long long* q_song,
+                                                      long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
+                                                      unsigned* heard, int blo, int bhi) {
   const int tid = threadIdx.x;
-  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
-  __syncthreads();
-
-  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
     int len = 0;
     if (tid < n) {
-      const int s2 = p.te_songs[base + tid];
-      const long long lo = p.trs_off[s2];
-      len = (int)(p.trs_off[s2 + 1] - lo);
+      const int s2 = te_songs[base + tid];
+      const long long lo = trs_off[s2];
+      len = (int)(trs_off[s2 + 1] - lo);
       s_lo[tid] = lo;
-      s_w[tid] = (MODEL == MR_IBM) ? p.q_song[s2] : 1ll;
+      s_w[tid] = (MODEL == MR_IBM) ? q_song[s2] : 1ll;
+      if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
     }
     int total;
     const int pre = block_excl_scan(len, &total, s_scan);
     s_pre[tid] = pre;
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
-    // Flattened walk over the listener lists L_tr(s2), s2 in this chunk of T(u).
     for (int i = tid; i < total; i += kThreads) {
-      int a = 0, b = n;  // find j with s_pre[j] <= i < s_pre[j+1]
+      int a = 0, b = n;  // j with s_pre[j] <= i < s_pre[j+1]
       while (b - a > 1) {
         const int m = (a + b) >> 1;
         if (s_pre[m] <= i) a = m; else b = m;
       }
-      const int v = p.trs_users[s_lo[a] + (i - s_pre[a])];
+      const int v = trs_users[s_lo[a] + (i - s_pre[a])];
       atomicAdd(&Y[v], (unsigned long long)s_w[a]);
     }
     __syncthreads();
   }
+}
 
-  // Compact the non-zero neighbours in train-user order.
+// Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
+// distinct-overlap count into the fixed-point cosine (MR:142-148).
+template <int MODEL>
+__device__ __forceinline__ long long neighbour_weight(unsigned long long y, double rs_u, double sqrt_tr_v,
+                                                      double two_f) {
+  if (MODEL == MR_IBM) return (long long)y;
+  const double c = (double)(long long)y / (rs_u * sqrt_tr_v);
+  return (long long)rint(c * two_f);
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw);         // [n_tr]
+  long long* s_lo = reinterpret_cast<long long*>(smem_raw + align16(p.n_tr * 8));  // [256]
+  long long* s_w = s_lo + kThreads;                                                // [256]
+  int* s_pre = reinterpret_cast<int*>(s_w + kThreads);                             // [257]
+  int* s_scan = s_pre + kThreads + 4;                                              // [kWaves]
+
+  const int bu = blockIdx.x;
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+  __syncthreads();
+  accumulate_neighbours<MODEL>(Y, p.te_off[u], p.te_off[u + 1], p.te_songs, p.trs_off, p.trs_users, p.q_song,
+                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0);
+
   const double two_f = ldexp(1.0, p.frac_bits);
   const double rs_u = p.sqrt_te[u];
   int* out_v = p.nbr_v + (size_t)bu * p.cap;
@@ -232,16 +326,8 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
     int total;
     const int pos = block_excl_scan(flag, &total, s_scan);
     if (flag) {
-      long long q;
-      if (MODEL == MR_IBM) {
-        q = (long long)y;
-      } else {
-        // cos_u = o / (sqrt|T(u)| * sqrt|S(v)|)  (MR:142-148), in fixed point.
-        const double c = (double)(long long)y / (rs_u * p.sqrt_tr[v]);
-        q = (long long)rint(c * two_f);
-      }
       out_v[written + pos] = v;
-      out_q[written + pos] = q;
+      out_q[written + pos] = neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
     }
     written += total;
   }
@@ -249,36 +335,53 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// stage 2: per (song tile, test user) LDS accumulation + dense epilogue +
-// per-tile top-k candidates. MR:159-166 (ubm rank), MR:249-257 (ibm rank),
-// MR:105-111 (pair enumeration; heard songs get NaN instead of no pair).
+// stage 2 (+ fused stage 1, + stage 3): one workgroup per (song tile, test
+// user). MR:159-166 (ubm rank), MR:249-257 (ibm rank), MR:105-111 (pairs).
 // ---------------------------------------------------------------------------
 struct ScoreParams {
+  int n_tr;
   int user0;
   int song_lo, song_hi, width;   // shard [lo, hi), width = hi - lo
   int block_songs, n_tiles;
-  int cap, frac_bits, topk, dense;
+  int frac_bits, topk, dense, merge_cap;
   const long long* te_off;
   const int* te_songs;
   const int* tr_songs;           // train u -> s column ids
   const int* blk_ptr;            // [n_tr][n_tiles+1] index into tr_songs
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
+  // fused stage 1 inputs
+  const long long* trs_off;
+  const int* trs_users;
+  const long long* q_song;
+  const double* sqrt_tr;
+  const double* sqrt_te;
+  // separate stage 1 outputs
+  int cap;
   const int* nbr_v;
   const long long* nbr_q;
   const int* nbr_cnt;
+  // outputs
   void* dense_out;               // [n_te][width] float or double
-  long long* cand_key;           // [batch][n_tiles][k]
+  long long* cand_key;           // [n_te][n_tiles][k] tile candidates
   int* cand_song;
+  unsigned* counter;             // [n_te] tiles finished (reset by the last tile)
+  long long* top_key;            // [n_te][k]
+  int* top_song;
+  double* top_score;
 };
 
-template <int MODEL, typename OutT>
+template <int MODEL, typename OutT, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
-  extern __shared__ unsigned long long smem[];
+  extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
-  unsigned long long* acc = smem;                                   // [bs]
-  unsigned* heard = reinterpret_cast<unsigned*>(acc + bs);          // [bs/32]
-  long long* sk = reinterpret_cast<long long*>(heard + bs / 32);    // [kWaves]
-  int* ss = reinterpret_cast<int*>(sk + kWaves);                    // [kWaves]
+  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.merge_cap);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
+  unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
+  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
+  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
+  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
+  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
+  int* flag = reinterpret_cast<int*>(smem_raw + L.flag);
 
   const int tile = blockIdx.x;
   const int bu = blockIdx.y;
@@ -287,27 +390,48 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const int blo = p.song_lo + tile * bs;
   const int bhi = min(p.song_hi, blo + bs);
   const int bw = bhi - blo;
+  const int stride = p.n_tiles + 1;
+  const double two_f = ldexp(1.0, p.frac_bits);
 
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
-  __syncthreads();
-
   const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
-  for (long long i = t0 + tid; i < t1; i += kThreads) {
-    const int s = p.te_songs[i];
-    if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
-  }
 
-  const int cnt = p.nbr_cnt[bu];
-  const int* nv = p.nbr_v + (size_t)bu * p.cap;
-  const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-  const int stride = p.n_tiles + 1;
-  for (int k = tid; k < cnt; k += kThreads) {
-    const int v = nv[k];
-    const unsigned long long q = (unsigned long long)nq[k];
-    const int* bp = p.blk_ptr + (size_t)v * stride + tile;
-    const int a = bp[0], b = bp[1];
-    for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+  if (FUSED) {
+    unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
+    for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+    __syncthreads();
+    accumulate_neighbours<MODEL>(Y, t0, t1, p.te_songs, p.trs_off, p.trs_users, p.q_song,
+                                 reinterpret_cast<long long*>(smem_raw + L.s_lo),
+                                 reinterpret_cast<long long*>(smem_raw + L.s_w),
+                                 reinterpret_cast<int*>(smem_raw + L.s_pre),
+                                 reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi);
+    const double rs_u = p.sqrt_te[u];
+    for (int v = tid; v < p.n_tr; v += kThreads) {
+      const unsigned long long y = Y[v];
+      if (y == 0ull) continue;
+      const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
+          y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
+      const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+      const int a = bp[0], b = bp[1];
+      for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+    }
+  } else {
+    __syncthreads();
+    for (long long i = t0 + tid; i < t1; i += kThreads) {
+      const int s = p.te_songs[i];
+      if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
+    }
+    const int cnt = p.nbr_cnt[bu];
+    const int* nv = p.nbr_v + (size_t)bu * p.cap;
+    const long long* nq = p.nbr_q + (size_t)bu * p.cap;
+    for (int k = tid; k < cnt; k += kThreads) {
+      const int v = nv[k];
+      const unsigned long long q = (unsigned long long)nq[k];
+      const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+      const int a = bp[0], b = bp[1];
+      for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+    }
   }
   __syncthreads();
 
@@ -321,23 +445,85 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
     acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
   }
-  if (p.topk <= 0) return;
+  const int k = p.topk;
+  if (k <= 0) return;
   __syncthreads();
-  long long* ck = p.cand_key + ((size_t)bu * p.n_tiles + tile) * p.topk;
-  int* cs = p.cand_song + ((size_t)bu * p.n_tiles + tile) * p.topk;
-  block_select_topk(
-      bw, p.topk,
+
+  // Tile top-k -> fk/fs (LDS).
+  block_topk(
+      bw,
       [&](int i, long long& key, int& song) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      ck, cs, sk, ss);
+      k, wk, ws, fk, fs);
+
+  if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
+    for (int r = tid; r < k; r += kThreads) {
+      const size_t o = (size_t)u * k + r;
+      p.top_key[o] = fk[r];
+      p.top_song[o] = fs[r];
+      p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+    }
+    return;
+  }
+
+  // Publish the tile's candidates (sc1), then count the tile in.
+  long long* ck = p.cand_key + (size_t)u * p.n_tiles * k;
+  int* cs = p.cand_song + (size_t)u * p.n_tiles * k;
+  for (int r = tid; r < k; r += kThreads) {
+    st_sc1(&ck[(size_t)tile * k + r], fk[r]);
+    st_sc1(&cs[(size_t)tile * k + r], fs[r]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(&p.counter[u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (old == (unsigned)(p.n_tiles - 1));
+  }
+  __syncthreads();
+  if (!*flag) return;
+
+  // Last tile of user u: merge all tiles' candidates (sc1 loads), staged in
+  // LDS region A, merge_cap entries per pass with the running best appended.
+  long long* mk = reinterpret_cast<long long*>(smem_raw + L.acc);
+  int* ms = reinterpret_cast<int*>(smem_raw + L.acc + p.merge_cap * 8);
+  const int n = p.n_tiles * k;
+  int done = 0, prev = 0;
+  while (true) {
+    const int take = min(n - done, p.merge_cap - prev);
+    for (int i = tid; i < take; i += kThreads) {
+      mk[i] = ld_sc1(&ck[done + i]);
+      ms[i] = ld_sc1(&cs[done + i]);
+    }
+    for (int i = tid; i < prev; i += kThreads) {
+      mk[take + i] = fk[i];
+      ms[take + i] = fs[i];
+    }
+    __syncthreads();
+    block_topk(
+        take + prev,
+        [&](int i, long long& key, int& song) {
+          key = mk[i];
+          song = ms[i];
+        },
+        k, wk, ws, fk, fs);
+    done += take;
+    prev = k;
+    if (done >= n) break;
+  }
+  for (int r = tid; r < k; r += kThreads) {
+    const size_t o = (size_t)u * k + r;
+    p.top_key[o] = fk[r];
+    p.top_song[o] = fs[r];
+    p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+  }
+  if (tid == 0) p.counter[u] = 0u;  // ready for the next launch (kernel boundary orders it)
 }
 
 // ---------------------------------------------------------------------------
-// stage 3: top-k merge over lists. Element (u, l, r) of the input sits at
-// u*user_stride + l*list_stride + r. Used for the per-tile candidates of one
-// context and for the per-shard lists after the all-gather.
+// Top-k merge over lists (exchange step after a song-shard all-gather).
+// Element (u, l, r) of the input sits at u*user_stride + l*list_stride + r.
 // ---------------------------------------------------------------------------
 struct MergeParams {
   int n_lists, k_in, k_out;
@@ -347,32 +533,30 @@ struct MergeParams {
   long long* out_keys;    // [n_users][k_out]
   int* out_songs;
   double* out_scores;     // may be null
-  long long out_user0;    // output row offset
 };
 
 __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
-  __shared__ long long sk[kWaves];
-  __shared__ int ss[kWaves];
-  __shared__ long long wk[kMaxTopK];
-  __shared__ int ws[kMaxTopK];
+  __shared__ long long wk[kWaves * kMaxTopK];
+  __shared__ int ws[kWaves * kMaxTopK];
+  __shared__ long long fk[kMaxTopK];
+  __shared__ int fs[kMaxTopK];
   const int bu = blockIdx.x;
   const long long* keys = p.keys + (size_t)bu * p.user_stride;
   const int* songs = p.songs + (size_t)bu * p.user_stride;
-  block_select_topk(
-      p.n_lists * p.k_in, p.k_out,
+  block_topk(
+      p.n_lists * p.k_in,
       [&](int i, long long& key, int& song) {
         const int l = i / p.k_in, r = i - l * p.k_in;
         const size_t off = (size_t)l * p.list_stride + r;
         key = keys[off];
         song = songs[off];
       },
-      wk, ws, sk, ss);
-  __syncthreads();
-  const size_t o = (size_t)(p.out_user0 + bu) * p.k_out;
+      p.k_out, wk, ws, fk, fs);
+  const size_t o = (size_t)bu * p.k_out;
   for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
-    p.out_keys[o + r] = wk[r];
-    p.out_songs[o + r] = ws[r];
-    if (p.out_scores) p.out_scores[o + r] = wk[r] >= 0 ? __longlong_as_double(wk[r]) : (double)NAN;
+    p.out_keys[o + r] = fk[r];
+    p.out_songs[o + r] = fs[r];
+    if (p.out_scores) p.out_scores[o + r] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
   }
 }
 
@@ -407,6 +591,9 @@ int dev_upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t st) {
   return MR_OK;
 }
 
+using ScoreKernel = void (*)(ScoreParams);
+using NbrKernel = void (*)(NbrParams);
+
 }  // namespace
 
 struct mr_ctx {
@@ -414,22 +601,27 @@ struct mr_ctx {
   hipStream_t stream = nullptr;
   bool loaded = false;
   bool ran = false;
+  bool fused = false;
   int last_model = -1;
   int n_tr = 0, n_te = 0, n_s = 0;
   int song_lo = 0, song_hi = 0, width = 0;
-  int block_songs = 0, n_tiles = 0;
+  int block_songs = 0, n_tiles = 0, merge_cap = 0;
   int cap = 0, batch = 0;
+  size_t score_lds = 0, nbr_lds = 0;
+  ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
+  NbrKernel nbr_kernel[2] = {nullptr, nullptr};
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
   DevBuf<int> tr_songs, te_songs, trs_users, blk_ptr, nbr_v, nbr_cnt, cand_song, top_song;
+  DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
   DevBuf<unsigned char> dense;
-  // Kernel timing ring: 4 events per timed batch (before stage 1, between
-  // stages, after stage 3), recorded without host synchronisation and
-  // resolved in flush_timing (mr_kernel_times, ring full, mr_load/destroy).
+  // Kernel timing ring: 3 events per timed batch (before stage 1, before the
+  // score kernel, after it), recorded without host synchronisation and
+  // resolved in flush_timing (mr_kernel_times, ring full).
   static constexpr int kRing = 1024;
   std::vector<hipEvent_t> ring;
   int ring_used = 0;
-  bool ring_has_merge[kRing] = {};
+  bool ring_has_stage1[kRing] = {};
   long long launches[3] = {0, 0, 0};
   double ms[3] = {0, 0, 0};
 
@@ -438,6 +630,7 @@ struct mr_ctx {
     cand_key.release(); top_key.release(); nbr_q.release();
     tr_songs.release(); te_songs.release(); trs_users.release(); blk_ptr.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
+    counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
     dense.release();
     loaded = ran = false;
@@ -463,23 +656,25 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
   return MR_OK;
 }
 
-int auto_block_songs(int width, int n_te) {
-  // Aim for >= ~1024 workgroups in stage 2, tiles of 256..16384 songs.
+int auto_block_songs(int width, int n_te, bool fused) {
+  // Aim for >= ~1024 workgroups, tiles of 256..16384 songs (fused: <= 8192,
+  // the neighbour array shares the LDS).
+  const long long cap = fused ? 8192 : kMaxBlockSongs;
   long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
   long long bs = ((want + 255) / 256) * 256;
-  bs = std::max<long long>(256, std::min<long long>(kMaxBlockSongs, bs));
+  bs = std::max<long long>(256, std::min<long long>(cap, bs));
   long long cover = ((long long)width + 255) / 256 * 256;  // no point in a tile wider than the shard
   return (int)std::max<long long>(256, std::min(bs, cover));
 }
 
-int launch_merge(hipStream_t st, int n_users, int n_lists, int k_in, int k_out, long long user_stride,
-                 long long list_stride, const long long* keys, const int* songs, long long* out_keys,
-                 int* out_songs, double* out_scores, long long out_user0) {
-  MergeParams mp{n_lists, k_in, k_out, user_stride, list_stride, keys, songs, out_keys, out_songs,
-                 out_scores, out_user0};
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_users), dim3(kThreads), 0, st, mp);
-  MR_HIP(hipGetLastError());
-  return MR_OK;
+template <int MODEL>
+void pick_kernels(mr_ctx* c) {
+  const bool f64 = c->opt.out_dtype == MR_OUT_F64;
+  if (c->fused)
+    c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, true> : k_score<MODEL, float, true>;
+  else
+    c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
+  c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
 }
 
 }  // namespace
@@ -487,7 +682,7 @@ int launch_merge(hipStream_t st, int n_users, int n_lists, int k_in, int k_out, 
 extern "C" {
 
 const char* mr_last_error(void) { return g_err.c_str(); }
-const char* mr_version(void) { return "mr_engine 0.1 (gfx950)"; }
+const char* mr_version(void) { return "mr_engine 0.2 (gfx950)"; }
 
 int mr_options_default(mr_options* opt) {
   if (!opt) return fail(MR_E_INVALID, "null options");
@@ -501,6 +696,7 @@ int mr_options_default(mr_options* opt) {
   opt->topk = 10;
   opt->dense = 1;
   opt->time_kernels = 0;
+  opt->stage1 = 0;
   return MR_OK;
 }
 
@@ -514,6 +710,7 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.out_dtype != MR_OUT_F32 && o.out_dtype != MR_OUT_F64) return fail(MR_E_INVALID, "bad out_dtype %d", o.out_dtype);
   if (o.block_songs < 0 || o.block_songs > kMaxBlockSongs || (o.block_songs % 256) != 0)
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
+  if (o.stage1 < 0 || o.stage1 > 2) return fail(MR_E_INVALID, "stage1 %d outside [0,2]", o.stage1);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   int ndev = 0;
   MR_HIP(hipGetDeviceCount(&ndev));
@@ -527,7 +724,7 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
     return fail(MR_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   if (o.time_kernels) {
-    c->ring.resize((size_t)mr_ctx::kRing * 4);
+    c->ring.resize((size_t)mr_ctx::kRing * 3);
     for (auto& ev : c->ring) {
       e = hipEventCreate(&ev);
       if (e != hipSuccess) {
@@ -597,12 +794,18 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     for (int v = 0; v < n_tr; ++v)
       for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) trs_users[fill[d->tr_songs[i]]++] = v;
   }
-  // Shard geometry.
+  // Shard geometry and launch shape.
   const int lo = c->opt.song_lo, hi = c->opt.song_hi > 0 ? c->opt.song_hi : n_s;
   if (lo < 0 || hi > n_s || lo >= hi) return fail(MR_E_INVALID, "song shard [%d,%d) invalid for %d songs", lo, hi, n_s);
   const int width = hi - lo;
-  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te);
+  const bool fused = c->opt.stage1 == 1 || (c->opt.stage1 == 0 && n_tr <= kMaxFusedTrainUsers);
+  if (fused && n_tr > kMaxFusedTrainUsers)
+    return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
+  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused);
+  if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
   const int n_tiles = (width + bs - 1) / bs;
+  const int k = c->opt.topk;
+  const int merge_cap = k > 0 ? std::min(n_tiles * k, kMergeStage) : 0;
   // Per-song / per-user fixed-point tables, computed once on the host with
   // correctly rounded std::sqrt (java.lang.Math.sqrt semantics, MR:147/237).
   const int F = c->opt.frac_bits;
@@ -626,11 +829,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       blk_ptr[(size_t)v * (n_tiles + 1) + j] = (int32_t)(std::lower_bound(b, e, bound) - d->tr_songs);
     }
   }
-  // Test-user batch so the neighbour lists fit a device budget (8 GiB).
+  // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = std::max(1, n_tr);
-  const size_t per_user = (size_t)cap * 12;
   const size_t budget = (size_t)8 << 30;
-  const int batch = (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / per_user));
+  const int batch = fused ? n_te : (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / ((size_t)cap * 12)));
 
   hipStream_t st = c->stream;
   if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(d->tr_off), (size_t)n_tr + 1, st))) return rc;
@@ -644,24 +846,39 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
   if ((rc = dev_upload(c->blk_ptr, blk_ptr.data(), blk_ptr.size(), st))) return rc;
-  if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
-  if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
-  if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch))) return rc;
-  const int k = c->opt.topk;
+  if (!fused) {
+    if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
+    if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
+    if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch))) return rc;
+  }
   if (k > 0) {
-    if ((rc = dev_alloc(c->cand_key, (size_t)batch * n_tiles * k))) return rc;
-    if ((rc = dev_alloc(c->cand_song, (size_t)batch * n_tiles * k))) return rc;
+    if ((rc = dev_alloc(c->cand_key, (size_t)n_te * n_tiles * k))) return rc;
+    if ((rc = dev_alloc(c->cand_song, (size_t)n_te * n_tiles * k))) return rc;
     if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
     if ((rc = dev_alloc(c->top_song, (size_t)n_te * k))) return rc;
     if ((rc = dev_alloc(c->top_score, (size_t)n_te * k))) return rc;
+    if ((rc = dev_alloc(c->counter, (size_t)n_te))) return rc;
+    MR_HIP(hipMemsetAsync(c->counter.p, 0, (size_t)n_te * sizeof(unsigned), st));
   }
   const size_t esz = c->opt.out_dtype == MR_OUT_F64 ? 8 : 4;
   if ((rc = dev_alloc(c->dense, c->opt.dense ? (size_t)n_te * width * esz : 1))) return rc;
+
+  c->fused = fused;
+  pick_kernels<MR_UBM>(c);
+  pick_kernels<MR_IBM>(c);
+  c->score_lds = (size_t)score_lds(bs, fused ? n_tr : 0, merge_cap).total;
+  c->nbr_lds = (size_t)align16(n_tr * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
+  for (int m = 0; m < 2; ++m) {
+    MR_HIP(hipFuncSetAttribute((const void*)c->score_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->score_lds));
+    MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->nbr_lds));
+  }
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
   c->song_lo = lo; c->song_hi = hi; c->width = width;
-  c->block_songs = bs; c->n_tiles = n_tiles;
+  c->block_songs = bs; c->n_tiles = n_tiles; c->merge_cap = merge_cap;
   c->cap = cap; c->batch = batch;
   c->loaded = true;
   c->ran = false;
@@ -677,74 +894,80 @@ int mr_shard_info(const mr_ctx* c, int32_t* lo, int32_t* hi, int32_t* n_te) {
   return MR_OK;
 }
 
+int mr_launch_info(const mr_ctx* c, int32_t* fused, int32_t* block_songs, int32_t* n_tiles) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_launch_info before mr_load");
+  if (fused) *fused = c->fused ? 1 : 0;
+  if (block_songs) *block_songs = c->block_songs;
+  if (n_tiles) *n_tiles = c->n_tiles;
+  return MR_OK;
+}
+
 }  // extern "C"
 
 namespace {
 
 int flush_timing(mr_ctx* c) {
   if (c->ring_used == 0) return MR_OK;
-  MR_HIP(hipEventSynchronize(c->ring[(size_t)(c->ring_used - 1) * 4 + 3]));
+  MR_HIP(hipEventSynchronize(c->ring[(size_t)(c->ring_used - 1) * 3 + 2]));
   for (int i = 0; i < c->ring_used; ++i) {
-    hipEvent_t* e = &c->ring[(size_t)i * 4];
+    hipEvent_t* e = &c->ring[(size_t)i * 3];
     float t;
-    MR_HIP(hipEventElapsedTime(&t, e[0], e[1])); c->ms[0] += t; c->launches[0]++;
+    if (c->ring_has_stage1[i]) { MR_HIP(hipEventElapsedTime(&t, e[0], e[1])); c->ms[0] += t; c->launches[0]++; }
     MR_HIP(hipEventElapsedTime(&t, e[1], e[2])); c->ms[1] += t; c->launches[1]++;
-    if (c->ring_has_merge[i]) { MR_HIP(hipEventElapsedTime(&t, e[2], e[3])); c->ms[2] += t; c->launches[2]++; }
   }
   c->ring_used = 0;
   return MR_OK;
 }
 
-template <int MODEL>
-int run_model(mr_ctx* c) {
+int run_model(mr_ctx* c, int model) {
   hipStream_t st = c->stream;
   const bool timed = c->opt.time_kernels != 0;
-  const size_t nbr_lds = (size_t)c->n_tr * 8 + kThreads * 16 + (kThreads + 1 + kWaves) * 4;
-  const size_t score_lds = (size_t)c->block_songs * 8 + (c->block_songs / 32) * 4 + kWaves * 12;
-  auto kn = k_neighbours<MODEL>;
-  MR_HIP(hipFuncSetAttribute((const void*)kn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nbr_lds));
-  void (*ks)(ScoreParams) =
-      c->opt.out_dtype == MR_OUT_F64 ? k_score<MODEL, double> : k_score<MODEL, float>;
-  MR_HIP(hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)score_lds));
   const int k = c->opt.topk;
   for (int user0 = 0; user0 < c->n_te; user0 += c->batch) {
     const int nb = std::min(c->batch, c->n_te - user0);
-    NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
-                 c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
-                 c->nbr_cnt.p};
     hipEvent_t* ev = nullptr;
     if (timed) {
       if (c->ring_used == mr_ctx::kRing) {
         int rc = flush_timing(c);
         if (rc) return rc;
       }
-      ev = &c->ring[(size_t)c->ring_used * 4];
-      c->ring_has_merge[c->ring_used] = k > 0;
+      ev = &c->ring[(size_t)c->ring_used * 3];
+      c->ring_has_stage1[c->ring_used] = !c->fused;
       c->ring_used++;
       MR_HIP(hipEventRecord(ev[0], st));
     }
-    hipLaunchKernelGGL(kn, dim3(nb), dim3(kThreads), nbr_lds, st, np);
-    MR_HIP(hipGetLastError());
+    if (!c->fused) {
+      NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
+                   c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
+                   c->nbr_cnt.p};
+      hipLaunchKernelGGL(c->nbr_kernel[model], dim3(nb), dim3(kThreads), c->nbr_lds, st, np);
+      MR_HIP(hipGetLastError());
+    }
     if (timed) MR_HIP(hipEventRecord(ev[1], st));
     for (int y0 = 0; y0 < nb; y0 += 65535) {
       const int ny = std::min(65535, nb - y0);
-      ScoreParams sp{user0 + y0, c->song_lo, c->song_hi, c->width, c->block_songs, c->n_tiles,
-                     c->cap, c->opt.frac_bits, k, c->opt.dense, c->te_off.p, c->te_songs.p,
-                     c->tr_songs.p, c->blk_ptr.p, c->sqrt_c.p,
-                     c->nbr_v.p + (size_t)y0 * c->cap, c->nbr_q.p + (size_t)y0 * c->cap,
-                     c->nbr_cnt.p + y0, c->dense.p,
-                     k > 0 ? c->cand_key.p + (size_t)y0 * c->n_tiles * k : nullptr,
-                     k > 0 ? c->cand_song.p + (size_t)y0 * c->n_tiles * k : nullptr};
-      hipLaunchKernelGGL(ks, dim3(c->n_tiles, ny), dim3(kThreads), score_lds, st, sp);
+      ScoreParams sp{};
+      sp.n_tr = c->n_tr;
+      sp.user0 = user0 + y0;
+      sp.song_lo = c->song_lo; sp.song_hi = c->song_hi; sp.width = c->width;
+      sp.block_songs = c->block_songs; sp.n_tiles = c->n_tiles;
+      sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense; sp.merge_cap = c->merge_cap;
+      sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
+      sp.tr_songs = c->tr_songs.p; sp.blk_ptr = c->blk_ptr.p; sp.sqrt_c = c->sqrt_c.p;
+      sp.trs_off = c->trs_off.p; sp.trs_users = c->trs_users.p; sp.q_song = c->q_song.p;
+      sp.sqrt_tr = c->sqrt_tr.p; sp.sqrt_te = c->sqrt_te.p;
+      sp.cap = c->cap;
+      sp.nbr_v = c->fused ? nullptr : c->nbr_v.p + (size_t)y0 * c->cap;
+      sp.nbr_q = c->fused ? nullptr : c->nbr_q.p + (size_t)y0 * c->cap;
+      sp.nbr_cnt = c->fused ? nullptr : c->nbr_cnt.p + y0;
+      sp.dense_out = c->dense.p;
+      sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
+      sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
+      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
     }
     if (timed) MR_HIP(hipEventRecord(ev[2], st));
-    if (k > 0) {
-      int rc = launch_merge(st, nb, c->n_tiles, k, k, (long long)c->n_tiles * k, k, c->cand_key.p,
-                            c->cand_song.p, c->top_key.p, c->top_song.p, c->top_score.p, user0);
-      if (rc) return rc;
-    }
-    if (timed) MR_HIP(hipEventRecord(ev[3], st));
   }
   return MR_OK;
 }
@@ -758,7 +981,7 @@ int mr_run(mr_ctx* c, int model) {
   if (!c->loaded) return fail(MR_E_STATE, "mr_run before mr_load");
   if (model != MR_UBM && model != MR_IBM) return fail(MR_E_INVALID, "unknown model %d", model);
   MR_HIP(hipSetDevice(c->opt.device));
-  int rc = model == MR_IBM ? run_model<MR_IBM>(c) : run_model<MR_UBM>(c);
+  int rc = run_model(c, model);
   if (rc) return rc;
   c->ran = true;
   c->last_model = model;
@@ -837,10 +1060,10 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
   if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
   MR_HIP(hipSetDevice(c->opt.device));
-  int rc = launch_merge(c->stream, n_te, n_shards, k, k, k, (long long)n_te * k,
-                        reinterpret_cast<const long long*>(keys_in), songs_in,
-                        reinterpret_cast<long long*>(keys_out), songs_out, scores_out, 0);
-  if (rc) return rc;
+  MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
+                 reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_te), dim3(kThreads), 0, c->stream, mp);
+  MR_HIP(hipGetLastError());
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
 }

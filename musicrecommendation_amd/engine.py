@@ -15,7 +15,7 @@ from . import _lib
 from .dataset import Dataset
 
 MODELS = {"ubm": _lib.MR_UBM, "ibm": _lib.MR_IBM, _lib.MR_UBM: _lib.MR_UBM, _lib.MR_IBM: _lib.MR_IBM}
-KERNELS = {"neighbours": 0, "score": 1, "merge": 2}
+KERNELS = {"neighbours": 0, "score": 1}
 
 
 def model_id(model: Union[str, int]) -> int:
@@ -28,7 +28,7 @@ def model_id(model: Union[str, int]) -> int:
 class Engine:
     def __init__(self, dataset: Dataset, *, device: int = 0, frac_bits: int = 32, song_lo: int = 0,
                  song_hi: int = 0, block_songs: int = 0, out_dtype: str = "f32", topk: int = 10,
-                 dense: bool = True, time_kernels: bool = False):
+                 dense: bool = True, time_kernels: bool = False, stage1: str = "auto"):
         self._L = _lib.lib()
         opt = _lib.MrOptions()
         _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
@@ -41,6 +41,7 @@ class Engine:
         opt.topk = topk
         opt.dense = 1 if dense else 0
         opt.time_kernels = 1 if time_kernels else 0
+        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2}[stage1]
         self.opt = opt
         self.dtype = np.float32 if out_dtype == "f32" else np.float64
         self._h = ctypes.c_void_p()
@@ -58,6 +59,10 @@ class Engine:
         self.song_lo, self.song_hi, self.n_test = lo.value, hi.value, nte.value
         self.width = self.song_hi - self.song_lo
         self.topk_k = topk
+        fz, bsz, nt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self._L.mr_launch_info(self._h, ctypes.byref(fz), ctypes.byref(bsz), ctypes.byref(nt)),
+                   "mr_launch_info")
+        self.fused, self.block_songs, self.n_tiles = bool(fz.value), bsz.value, nt.value
 
     # ---- lifecycle ----------------------------------------------------------
     def close(self) -> None:

@@ -70,11 +70,29 @@ def test_golden_fixture(name, model):
     assert rel_err(g32, z[model]) < 1e-5
 
 
-@pytest.mark.parametrize("block", [256, 512, 768, 16384])
+@pytest.mark.parametrize("stage1", ["fused", "separate"])
+@pytest.mark.parametrize("block", [256, 512, 768, 8192, 16384])
 @pytest.mark.parametrize("model", MODELS)
-def test_tile_sizes_bit_identical(block, model):
+def test_tile_sizes_bit_identical(block, model, stage1):
     ds, _ = synth_fixture("small")
-    check_exact(ds, model, block_songs=block)
+    if stage1 == "fused" and block > 8192:
+        with pytest.raises(_lib.EngineError):
+            Engine(ds, block_songs=block, stage1=stage1)
+        return
+    check_exact(ds, model, block_songs=block, stage1=stage1)
+
+
+def test_launch_shape_selection():
+    ds, _ = synth_fixture("small")
+    with Engine(ds) as e:
+        assert e.fused and e.n_tiles >= 2
+    with Engine(ds, stage1="separate", block_songs=256) as e:
+        assert not e.fused and e.block_songs == 256
+    big = synth.generate(4100, 3, 5, alpha=0.87).dataset()
+    with Engine(big) as e:
+        assert not e.fused
+    with pytest.raises(_lib.EngineError):
+        Engine(big, stage1="fused")
 
 
 @pytest.mark.parametrize("frac_bits", [16, 24, 40])
@@ -102,11 +120,30 @@ def test_topk_only_mode():
     assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
 
 
+@pytest.mark.parametrize("stage1", ["fused", "separate"])
 @pytest.mark.parametrize("name", ["c1", "c2"])
 @pytest.mark.parametrize("model", MODELS)
-def test_named_configs_exact(name, model):
+def test_named_configs_exact(name, model, stage1):
     ds = synth.config(name).dataset()
-    check_exact(ds, model)
+    check_exact(ds, model, stage1=stage1)
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_many_tiles_multi_pass_merge(model):
+    """n_tiles * k > 2048 candidates: the in-kernel merge runs several passes."""
+    ds = synth.config("c2").dataset()
+    check_exact(ds, model, k=64, block_songs=256)   # 66 tiles x 64 = 4224 candidates
+
+
+def test_repeated_runs_reuse_counters():
+    ds = synth.config("c2").dataset()
+    with Engine(ds, out_dtype="f64") as e:
+        e.run("ibm"); e.run("ubm"); e.run("ibm")
+        a = e.dense(); s1, _, k1 = e.topk()
+        e.run("ibm")
+        assert np.array_equal(a, e.dense(), equal_nan=True)
+        s2, _, k2 = e.topk()
+        assert np.array_equal(s1, s2) and np.array_equal(k1, k2)
 
 
 @pytest.mark.parametrize("model", MODELS)
