@@ -45,7 +45,6 @@ constexpr int kMaxTopK = 64;
 constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS is 160 KiB)
 constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64)
 constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live together
-constexpr int kMergeStage = 2048;         // candidates staged in LDS per merge pass
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
 
 thread_local std::string g_err = "no error";
@@ -86,31 +85,46 @@ namespace {
   } while (0)
 
 // ---------------------------------------------------------------------------
-// LDS layout of k_score (bytes; every region 16-byte aligned). Region A holds
-// the tile accumulators (+ the fused path's neighbour array Y) and is reused
-// as the merge staging area once the tile's own top-k has been published.
+// Top-k selection geometry. A wave ranks a chunk of C = 64*E candidates by
+// counting (every lane compares its candidates with all C, broadcast LDS
+// reads, no dependent shuffle chains) and keeps the chunk's k best; rounds
+// repeat over the survivors until one chunk is left. C must exceed k.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int sel_e(int k) { return k <= 16 ? 1 : (k <= 32 ? 2 : 4); }
+__host__ __device__ inline int sel_out(int n, int k) {  // survivors of one round over n candidates
+  const int c = 64 * sel_e(k);
+  return ((n + c - 1) / c) * k;
+}
+
+// ---------------------------------------------------------------------------
+// LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs, flag, sel_cap, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int merge_cap) {
+__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles) {
   ScoreLds L;
-  const int a = bs * 8 + fused_ntr * 8;
-  const int m = merge_cap * 12;
-  L.acc = 0;
-  L.y = bs * 8;
-  int o = align16(a > m ? a : m);
-  L.heard = o; o = align16(o + (bs / 32) * 4);
   const int fused = fused_ntr > 0 ? 1 : 0;
+  const int kk = k > 0 ? k : 1;
+  const int C = 64 * sel_e(kk);
+  const int out_tile = sel_out(bs, kk), out_merge = sel_out(n_tiles * kk, kk);
+  L.sel_cap = out_tile > out_merge ? out_tile : out_merge;
+  int o = 0;
+  L.acc = o; L.y = bs * 8; o = align16(bs * 8 + fused_ntr * 8);
+  L.heard = o; o = align16(o + (bs / 32) * 4);
   L.s_lo = o; o += fused * kThreads * 8;
   L.s_w = o; o += fused * kThreads * 8;
   L.s_pre = o; o = align16(o + (kThreads + 1) * 4);
   L.s_scan = o; o = align16(o + kWaves * 4);
-  L.wk = o; o = align16(o + kWaves * kMaxTopK * 8);
-  L.ws = o; o = align16(o + kWaves * kMaxTopK * 4);
+  L.slot_k = o; o = align16(o + kWaves * C * 8);
+  L.slot_s = o; o = align16(o + kWaves * C * 4);
+  L.a_k = o; o = align16(o + L.sel_cap * 8);
+  L.a_s = o; o = align16(o + L.sel_cap * 4);
+  L.b_k = o; o = align16(o + L.sel_cap * 8);
+  L.b_s = o; o = align16(o + L.sel_cap * 4);
   L.fk = o; o = align16(o + kMaxTopK * 8);
   L.fs = o; o = align16(o + kMaxTopK * 4);
   L.flag = o; o = align16(o + 4);
@@ -150,68 +164,100 @@ __device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, 
   return ka > kb || (ka == kb && sa < sb);
 }
 
-// Wave-wide best candidate (all 64 lanes return it); shuffles only, no LDS.
-__device__ __forceinline__ void wave_best(long long& k, int& s) {
+// Make a wave's LDS writes visible to the other lanes of the same wave (LDS
+// operations of one wave complete in order; the fences stop the compiler
+// from moving the accesses across).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kMaxE = 4;
+
+// One selection round: chunk c of C = 64*E consecutive candidates (wave c mod
+// 4 owns it) -> its k best in (key desc, song asc) order at out[c*k .. c*k+k),
+// missing slots (-1, -1). get(i, key, song) reads candidate i < n; key < 0 =
+// not a candidate. A candidate's slot is its rank = the number of chunk
+// candidates before it in the total order (ranks of distinct songs are distinct).
+template <typename Get>
+__device__ __forceinline__ void select_round(int n, int k, Get get, long long* slot_k, int* slot_s, long long* out_k,
+                                             int* out_s) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int E = sel_e(k), C = 64 * E;
+  const int nchunks = (n + C - 1) / C;
+  long long* sk = slot_k + w * C;
+  int* ss = slot_s + w * C;
+  for (int c = w; c < nchunks; c += kWaves) {
+    const int base = c * C;
+    const int cnt = min(C, n - base);
+    long long key[kMaxE];
+    int song[kMaxE];
+    int nvalid = 0;
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    const long long ko = __shfl_xor(k, m, 64);
-    const int so = __shfl_xor(s, m, 64);
-    if (cand_before(ko, so, k, s)) { k = ko; s = so; }
-  }
-}
-
-// One wave selects its top-k: round r takes the best candidate strictly after
-// round r-1's winner in the total order (candidates are distinct songs, so no
-// "taken" marks). Lane l supplies m_l candidates via get(j, key, song); key < 0
-// = no candidate. Lane 0 writes out_k/out_s[0..k); missing slots -> (-1, -1).
-template <typename Get>
-__device__ __forceinline__ void wave_topk(int m, Get get, int k, long long* out_k, int* out_s) {
-  const int lane = threadIdx.x & 63;
-  long long pk = LLONG_MAX;
-  int ps = -1;
-  int r = 0;
-  for (; r < k; ++r) {
-    long long bk = kKeyNone;
-    int bs = INT_MAX;
-    for (int j = 0; j < m; ++j) {
-      long long ck;
-      int cs;
-      get(j, ck, cs);
-      if (ck >= 0 && cand_before(pk, ps, ck, cs) && cand_before(ck, cs, bk, bs)) { bk = ck; bs = cs; }
+    for (int e = 0; e < kMaxE; ++e) {
+      key[e] = kKeyNone;
+      song[e] = INT_MAX;
+      if (e < E) {
+        const int j = e * 64 + lane;
+        if (j < cnt) get(base + j, key[e], song[e]);
+        if (key[e] < 0) { key[e] = kKeyNone; song[e] = INT_MAX; }
+        sk[j] = key[e];
+        ss[j] = song[e];
+        nvalid += __popcll(__ballot(key[e] >= 0));
+      }
     }
-    wave_best(bk, bs);  // wave-uniform from here
-    if (bk < 0) break;
-    if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
-    pk = bk;
-    ps = bs;
+    wave_lds_sync();
+    long long* ok = out_k + (size_t)c * k;
+    int* os = out_s + (size_t)c * k;
+#pragma unroll
+    for (int e = 0; e < kMaxE; ++e) {
+      if (e < E && key[e] >= 0) {
+        int rank = 0;
+        for (int j = 0; j < cnt; ++j) rank += cand_before(sk[j], ss[j], key[e], song[e]) ? 1 : 0;
+        if (rank < k) { ok[rank] = key[e]; os[rank] = song[e]; }
+      }
+    }
+    for (int r = nvalid + lane; r < k; r += 64) { ok[r] = kKeyNone; os[r] = -1; }
+    wave_lds_sync();  // the slot is rewritten by the wave's next chunk
   }
-  for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
 }
 
-// Block top-k over elements [0, n): wave w scans elements w*64+lane (+256 j),
-// then wave 0 selects from the 4 wave lists. Two barriers in total.
+// Block top-k of n candidates -> out_k/out_s[0..k) (LDS), sorted; rounds of
+// select_round over the survivors (buffers a/b hold sel_cap entries each).
+// Every thread of the block must call it; it ends with a barrier.
 template <typename Get>
-__device__ __forceinline__ void block_topk(int n, Get get, int k, long long* wk, int* ws, long long* out_k,
-                                           int* out_s) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int first = w * 64 + lane;
-  const int m = first < n ? (n - first + kThreads - 1) / kThreads : 0;
-  wave_topk(
-      m, [&](int j, long long& key, int& song) { get(first + j * kThreads, key, song); }, k, wk + w * k,
-      ws + w * k);
-  __syncthreads();
-  if (w == 0) {
-    const int tot = kWaves * k;
-    const int m0 = lane < tot ? (tot - lane + 63) / 64 : 0;
-    wave_topk(
-        m0,
-        [&](int j, long long& key, int& song) {
-          key = wk[lane + j * 64];
-          song = ws[lane + j * 64];
-        },
-        k, out_k, out_s);
+__device__ __forceinline__ void block_select(int n, int k, Get get, long long* slot_k, int* slot_s, long long* a_k,
+                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s) {
+  const int C = 64 * sel_e(k);
+  if (n <= C) {
+    select_round(n, k, get, slot_k, slot_s, out_k, out_s);
+    __syncthreads();
+    return;
   }
+  select_round(n, k, get, slot_k, slot_s, a_k, a_s);
+  int m = sel_out(n, k);
   __syncthreads();
+  long long* src_k = a_k;
+  int* src_s = a_s;
+  long long* dst_k = b_k;
+  int* dst_s = b_s;
+  while (true) {
+    auto from_src = [&](int i, long long& key, int& song) {
+      key = src_k[i];
+      song = src_s[i];
+    };
+    if (m <= C) {
+      select_round(m, k, from_src, slot_k, slot_s, out_k, out_s);
+      __syncthreads();
+      return;
+    }
+    select_round(m, k, from_src, slot_k, slot_s, dst_k, dst_s);
+    m = sel_out(m, k);
+    __syncthreads();
+    long long* tk = src_k; src_k = dst_k; dst_k = tk;
+    int* ts = src_s; src_s = dst_s; dst_s = ts;
+  }
 }
 
 // sc1 (L2-coherent, agent-scope) stores/loads for the in-launch hand-off of
@@ -343,7 +389,7 @@ struct ScoreParams {
   int user0;
   int song_lo, song_hi, width;   // shard [lo, hi), width = hi - lo
   int block_songs, n_tiles;
-  int frac_bits, topk, dense, merge_cap;
+  int frac_bits, topk, dense;
   const long long* te_off;
   const int* te_songs;
   const int* tr_songs;           // train u -> s column ids
@@ -374,11 +420,15 @@ template <int MODEL, typename OutT, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
-  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.merge_cap);
+  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
-  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
-  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
+  long long* slot_k = reinterpret_cast<long long*>(smem_raw + L.slot_k);
+  int* slot_s = reinterpret_cast<int*>(smem_raw + L.slot_s);
+  long long* a_k = reinterpret_cast<long long*>(smem_raw + L.a_k);
+  int* a_s = reinterpret_cast<int*>(smem_raw + L.a_s);
+  long long* b_k = reinterpret_cast<long long*>(smem_raw + L.b_k);
+  int* b_s = reinterpret_cast<int*>(smem_raw + L.b_s);
   long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   int* flag = reinterpret_cast<int*>(smem_raw + L.flag);
@@ -450,13 +500,13 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   __syncthreads();
 
   // Tile top-k -> fk/fs (LDS).
-  block_topk(
-      bw,
+  block_select(
+      bw, k,
       [&](int i, long long& key, int& song) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      k, wk, ws, fk, fs);
+      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
     for (int r = tid; r < k; r += kThreads) {
@@ -484,34 +534,14 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   __syncthreads();
   if (!*flag) return;
 
-  // Last tile of user u: merge all tiles' candidates (sc1 loads), staged in
-  // LDS region A, merge_cap entries per pass with the running best appended.
-  long long* mk = reinterpret_cast<long long*>(smem_raw + L.acc);
-  int* ms = reinterpret_cast<int*>(smem_raw + L.acc + p.merge_cap * 8);
-  const int n = p.n_tiles * k;
-  int done = 0, prev = 0;
-  while (true) {
-    const int take = min(n - done, p.merge_cap - prev);
-    for (int i = tid; i < take; i += kThreads) {
-      mk[i] = ld_sc1(&ck[done + i]);
-      ms[i] = ld_sc1(&cs[done + i]);
-    }
-    for (int i = tid; i < prev; i += kThreads) {
-      mk[take + i] = fk[i];
-      ms[take + i] = fs[i];
-    }
-    __syncthreads();
-    block_topk(
-        take + prev,
-        [&](int i, long long& key, int& song) {
-          key = mk[i];
-          song = ms[i];
-        },
-        k, wk, ws, fk, fs);
-    done += take;
-    prev = k;
-    if (done >= n) break;
-  }
+  // Last tile of user u: top-k over all tiles' candidates (sc1 loads).
+  block_select(
+      p.n_tiles * k, k,
+      [&](int i, long long& key, int& song) {
+        key = ld_sc1(&ck[i]);
+        song = ld_sc1(&cs[i]);
+      },
+      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
   for (int r = tid; r < k; r += kThreads) {
     const size_t o = (size_t)u * k + r;
     p.top_key[o] = fk[r];
@@ -535,23 +565,38 @@ struct MergeParams {
   double* out_scores;     // may be null
 };
 
+__host__ __device__ inline int merge_lds_bytes(int n, int k) {
+  const int C = 64 * sel_e(k);
+  const int cap = sel_out(n, k);
+  return align16(kWaves * C * 12) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
+}
+
 __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
-  __shared__ long long wk[kWaves * kMaxTopK];
-  __shared__ int ws[kWaves * kMaxTopK];
-  __shared__ long long fk[kMaxTopK];
-  __shared__ int fs[kMaxTopK];
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int k = p.k_out;
+  const int n = p.n_lists * p.k_in;
+  const int C = 64 * sel_e(k);
+  const int cap = sel_out(n, k);
+  long long* slot_k = reinterpret_cast<long long*>(smem_raw);
+  int* slot_s = reinterpret_cast<int*>(slot_k + kWaves * C);
+  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 12));
+  int* a_s = reinterpret_cast<int*>(a_k + cap);
+  long long* b_k = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(a_k) + align16(cap * 12));
+  int* b_s = reinterpret_cast<int*>(b_k + cap);
+  long long* fk = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(b_k) + align16(cap * 12));
+  int* fs = reinterpret_cast<int*>(fk + kMaxTopK);
   const int bu = blockIdx.x;
   const long long* keys = p.keys + (size_t)bu * p.user_stride;
   const int* songs = p.songs + (size_t)bu * p.user_stride;
-  block_topk(
-      p.n_lists * p.k_in,
+  block_select(
+      n, k,
       [&](int i, long long& key, int& song) {
         const int l = i / p.k_in, r = i - l * p.k_in;
         const size_t off = (size_t)l * p.list_stride + r;
         key = keys[off];
         song = songs[off];
       },
-      p.k_out, wk, ws, fk, fs);
+      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
   const size_t o = (size_t)bu * p.k_out;
   for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
     p.out_keys[o + r] = fk[r];
@@ -605,7 +650,7 @@ struct mr_ctx {
   int last_model = -1;
   int n_tr = 0, n_te = 0, n_s = 0;
   int song_lo = 0, song_hi = 0, width = 0;
-  int block_songs = 0, n_tiles = 0, merge_cap = 0;
+  int block_songs = 0, n_tiles = 0;
   int cap = 0, batch = 0;
   size_t score_lds = 0, nbr_lds = 0;
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
@@ -805,7 +850,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
   const int n_tiles = (width + bs - 1) / bs;
   const int k = c->opt.topk;
-  const int merge_cap = k > 0 ? std::min(n_tiles * k, kMergeStage) : 0;
   // Per-song / per-user fixed-point tables, computed once on the host with
   // correctly rounded std::sqrt (java.lang.Math.sqrt semantics, MR:147/237).
   const int F = c->opt.frac_bits;
@@ -866,7 +910,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->fused = fused;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
-  c->score_lds = (size_t)score_lds(bs, fused ? n_tr : 0, merge_cap).total;
+  c->score_lds = (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles).total;
+  if (c->score_lds > 160 * 1024)
+    return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
+                c->score_lds);
   c->nbr_lds = (size_t)align16(n_tr * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
   for (int m = 0; m < 2; ++m) {
     MR_HIP(hipFuncSetAttribute((const void*)c->score_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -878,7 +925,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
 
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
   c->song_lo = lo; c->song_hi = hi; c->width = width;
-  c->block_songs = bs; c->n_tiles = n_tiles; c->merge_cap = merge_cap;
+  c->block_songs = bs; c->n_tiles = n_tiles;
   c->cap = cap; c->batch = batch;
   c->loaded = true;
   c->ran = false;
@@ -952,7 +999,7 @@ int run_model(mr_ctx* c, int model) {
       sp.user0 = user0 + y0;
       sp.song_lo = c->song_lo; sp.song_hi = c->song_hi; sp.width = c->width;
       sp.block_songs = c->block_songs; sp.n_tiles = c->n_tiles;
-      sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense; sp.merge_cap = c->merge_cap;
+      sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.tr_songs = c->tr_songs.p; sp.blk_ptr = c->blk_ptr.p; sp.sqrt_c = c->sqrt_c.p;
       sp.trs_off = c->trs_off.p; sp.trs_users = c->trs_users.p; sp.q_song = c->q_song.p;
@@ -1062,7 +1109,10 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   MR_HIP(hipSetDevice(c->opt.device));
   MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
                  reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_te), dim3(kThreads), 0, c->stream, mp);
+  const int lds = merge_lds_bytes(n_shards * k, k);
+  if (lds > 160 * 1024) return fail(MR_E_INVALID, "merge of %d lists x %d needs too much LDS", n_shards, k);
+  MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipLaunchKernelGGL(k_topk_merge, dim3(n_te), dim3(kThreads), lds, c->stream, mp);
   MR_HIP(hipGetLastError());
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
