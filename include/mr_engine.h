@@ -179,6 +179,11 @@ int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
  * timed launches and their summed device milliseconds; reset=1 clears. */
 int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
 
+/* Diagnostic builds only (libmr_engine_stamps.so, -DMR_STAMPS): copy the
+ * per-workgroup phase timestamps of the last scoring launch ([grid][8]
+ * s_memrealtime values); MR_E_STATE in the production build. */
+int mr_debug_stamps(mr_ctx* ctx, int64_t* out, int64_t n);
+
 /* HIP stream of the context (as void* = hipStream_t). */
 void* mr_stream(const mr_ctx* ctx);
 

@@ -15,7 +15,9 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmr_engine.so")
+# MR_ENGINE_LIB=stamps selects the diagnostic build (phase timestamps).
+LIB_PATH = os.path.join(_HERE, "libmr_engine_stamps.so" if os.environ.get("MR_ENGINE_LIB") == "stamps"
+                        else "libmr_engine.so")
 
 MR_OK = 0
 MR_E_INVALID = -1
@@ -96,6 +98,7 @@ SIGNATURES = {
     "mr_topk_merge_host": (c_int, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_topk_merge_device": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),
+    "mr_debug_stamps": (c_int, [c_void_p, c_void_p, c_int64]),
     "mr_stream": (c_void_p, [c_void_p]),
     "mr_last_error": (c_char_p, []),
     "mr_corpus_from_tsv": (c_int, [c_char_p, c_char_p, c_char_p, POINTER(c_void_p)]),

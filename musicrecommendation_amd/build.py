@@ -39,15 +39,24 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return OUT
+OUT_STAMPS = os.path.join(HERE, "libmr_engine_stamps.so")
+
+
+def _compile(out: str, extra, verbose: bool) -> None:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, f"-I{INCLUDE}", *sources(), "-o", OUT + ".tmp"]
+    cmd = [hipcc, *FLAGS, *extra, f"-I{INCLUDE}", *sources(), "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(out + ".tmp", out)
+
+
+def build(force: bool = False, verbose: bool = False, stamps: bool = True) -> str:
+    """Production library; plus the phase-timestamp diagnostic variant."""
+    if force or _stale():
+        _compile(OUT, [], verbose)
+        if stamps:
+            _compile(OUT_STAMPS, ["-DMR_STAMPS"], verbose)
     return OUT
 
 

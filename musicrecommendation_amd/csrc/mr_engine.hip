@@ -136,6 +136,20 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
 // device helpers
 // ---------------------------------------------------------------------------
 
+// Diagnostic build only (-DMR_STAMPS, libmr_engine_stamps.so): thread 0 of
+// each scoring workgroup records s_memrealtime (100 MHz) at phase boundaries
+// into a debug buffer; the production build compiles these away.
+#ifdef MR_STAMPS
+#define MR_STAMP(i)                                                                     \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && p.stamps)                                                   \
+      p.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] =                \
+          (long long)__builtin_amdgcn_s_memrealtime();                                  \
+  } while (0)
+#else
+#define MR_STAMP(i) do {} while (0)
+#endif
+
 // Block-wide exclusive scan of one int per thread (256 threads). `sbuf` holds kWaves ints.
 __device__ __forceinline__ int block_excl_scan(int x, int* total, int* sbuf) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -414,6 +428,7 @@ struct ScoreParams {
   long long* top_key;            // [n_te][k]
   int* top_song;
   double* top_score;
+  long long* stamps;             // diagnostic build: [grid][8] phase timestamps
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -442,6 +457,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const int bw = bhi - blo;
   const int stride = p.n_tiles + 1;
   const double two_f = ldexp(1.0, p.frac_bits);
+  MR_STAMP(0);
 
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
@@ -456,6 +472,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
                                  reinterpret_cast<long long*>(smem_raw + L.s_w),
                                  reinterpret_cast<int*>(smem_raw + L.s_pre),
                                  reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi);
+    MR_STAMP(1);
     const double rs_u = p.sqrt_te[u];
     for (int v = tid; v < p.n_tr; v += kThreads) {
       const unsigned long long y = Y[v];
@@ -472,6 +489,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       const int s = p.te_songs[i];
       if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
     }
+    MR_STAMP(1);
     const int cnt = p.nbr_cnt[bu];
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
@@ -484,6 +502,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     }
   }
   __syncthreads();
+  MR_STAMP(2);
 
   // Epilogue: scores -> dense row segment; keys stay in LDS for the top-k.
   const double inv_f = ldexp(1.0, -p.frac_bits);
@@ -498,6 +517,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const int k = p.topk;
   if (k <= 0) return;
   __syncthreads();
+  MR_STAMP(3);
 
   // Tile top-k -> fk/fs (LDS).
   block_select(
@@ -507,6 +527,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         song = blo + i;
       },
       slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
+  MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
     for (int r = tid; r < k; r += kThreads) {
@@ -532,6 +553,14 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     *flag = (old == (unsigned)(p.n_tiles - 1));
   }
   __syncthreads();
+  MR_STAMP(5);
+#ifdef MR_STAMPS
+  if (tid == 0 && p.stamps) {
+    const size_t sb = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    p.stamps[sb + 6] = p.stamps[sb + 5];
+    p.stamps[sb + 7] = (long long)(*flag) | ((long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 8);
+  }
+#endif
   if (!*flag) return;
 
   // Last tile of user u: top-k over all tiles' candidates (sc1 loads).
@@ -549,6 +578,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
   }
   if (tid == 0) p.counter[u] = 0u;  // ready for the next launch (kernel boundary orders it)
+  MR_STAMP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -660,6 +690,7 @@ struct mr_ctx {
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
   DevBuf<unsigned char> dense;
+  DevBuf<long long> stamps;
   // Kernel timing ring: 3 events per timed batch (before stage 1, before the
   // score kernel, after it), recorded without host synchronisation and
   // resolved in flush_timing (mr_kernel_times, ring full).
@@ -678,6 +709,7 @@ struct mr_ctx {
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
     dense.release();
+    stamps.release();
     loaded = ran = false;
   }
 };
@@ -701,10 +733,10 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
   return MR_OK;
 }
 
-int auto_block_songs(int width, int n_te, bool fused) {
-  // Aim for >= ~1024 workgroups, tiles of 256..16384 songs (fused: <= 8192,
-  // the neighbour array shares the LDS).
-  const long long cap = fused ? 8192 : kMaxBlockSongs;
+int auto_block_songs(int width, int n_te, bool fused, int k) {
+  // Aim for >= ~1024 workgroups, tiles of 256..8192 songs (16384 only
+  // without top-k: the selection buffers share the LDS with the tile).
+  const long long cap = (fused || k > 0) ? 8192 : kMaxBlockSongs;
   long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
   long long bs = ((want + 255) / 256) * 256;
   bs = std::max<long long>(256, std::min<long long>(cap, bs));
@@ -846,7 +878,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const bool fused = c->opt.stage1 == 1 || (c->opt.stage1 == 0 && n_tr <= kMaxFusedTrainUsers);
   if (fused && n_tr > kMaxFusedTrainUsers)
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
-  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused);
+  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, c->opt.topk);
   if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
   const int n_tiles = (width + bs - 1) / bs;
   const int k = c->opt.topk;
@@ -921,6 +953,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
   }
+#ifdef MR_STAMPS
+  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * 8))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * 8 * 8, st));
+#endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
@@ -1011,6 +1047,7 @@ int run_model(mr_ctx* c, int model) {
       sp.dense_out = c->dense.p;
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
+      sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * 8 : nullptr;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
     }
@@ -1116,6 +1153,16 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   MR_HIP(hipGetLastError());
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
+}
+
+int mr_debug_stamps(mr_ctx* c, int64_t* out, int64_t n) {
+  if (!c || !out) return fail(MR_E_INVALID, "null argument");
+  if (!c->stamps.p) return fail(MR_E_STATE, "library built without -DMR_STAMPS");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const size_t m = std::min<size_t>((size_t)n, c->stamps.n);
+  MR_HIP(hipMemcpyAsync(out, c->stamps.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return (int)MR_OK;
 }
 
 int mr_kernel_times(mr_ctx* c, int32_t which, int64_t* launches, double* total_ms, int32_t reset) {

@@ -1,0 +1,43 @@
+"""Phase timestamps of the scoring kernel (diagnostic build).
+Usage: python scripts/stamps.py [config] [model] [block_songs] [stage1]"""
+import os
+import sys
+
+os.environ["MR_ENGINE_LIB"] = "stamps"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+from musicrecommendation_amd import synth  # noqa: E402
+from musicrecommendation_amd.engine import Engine  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+model = sys.argv[2] if len(sys.argv) > 2 else "ibm"
+bs = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+stage1 = sys.argv[4] if len(sys.argv) > 4 else "auto"
+ds = synth.config(cfg).dataset()
+e = Engine(ds, block_songs=bs, stage1=stage1)
+for _ in range(20):
+    e.run(model)
+e.sync()
+n = e.n_tiles * ds.n_test
+buf = np.zeros(n * 8, dtype=np.int64)
+rc = e._L.mr_debug_stamps(e._h, buf.ctypes.data, buf.size)
+assert rc == 0, e._L.mr_last_error()
+st = buf.reshape(n, 8).astype(np.float64)
+t0 = st[:, 0].min()
+ns = 10.0  # s_memrealtime: 100 MHz
+names = ["start", "stage1", "stage2", "epilogue", "tile-topk", "handoff", "merge(last)"]
+print(f"{cfg} {model} fused={e.fused} bs={e.block_songs} tiles={e.n_tiles} WGs={n}")
+print("WG start offsets (us): min/med/max", *(np.percentile(st[:, 0] - t0, [0, 50, 100]) * ns / 1e3))
+for i in range(1, 6):
+    d = (st[:, i] - st[:, i - 1]) * ns / 1e3
+    print(f"  {names[i]:12s} us: med {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}  max {d.max():7.3f}")
+last = (st[:, 7].astype(np.int64) & 1) == 1
+d = (st[last, 6] - st[last, 5]) * ns / 1e3
+print(f"  {'merge(last)':12s} us: med {np.median(d):7.3f}  max {d.max():7.3f}  (n={last.sum()})")
+end = np.where(last, st[:, 6], st[:, 5])
+print("WG end offsets (us): min/med/max", *(np.percentile(end - t0, [0, 50, 100]) * ns / 1e3))
+xcc = (st[:, 7].astype(np.int64) >> 8) & 15
+print("WGs per XCC:", np.bincount(xcc, minlength=8).tolist())
