@@ -100,11 +100,16 @@ __host__ __device__ inline int sel_out(int n, int k) {  // survivors of one roun
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs, flag, sel_cap, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot, a_k, a_s, b_k, b_s, fk, fs, flag, sel_cap, stage_cap, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
+constexpr int kMergeStageMax = 2048;  // tile candidates staged in LDS for the in-launch merge
+
+// Region A (offset 0) first holds the tile accumulators (+ the fused path's
+// neighbour array Y); once the tile's own top-k is out it is reused to stage
+// the user's tile candidates for the merge (stage_cap entries: keys, songs).
 __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles) {
   ScoreLds L;
   const int fused = fused_ntr > 0 ? 1 : 0;
@@ -112,15 +117,18 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   const int C = 64 * sel_e(kk);
   const int out_tile = sel_out(bs, kk), out_merge = sel_out(n_tiles * kk, kk);
   L.sel_cap = out_tile > out_merge ? out_tile : out_merge;
+  const int nc = n_tiles * kk;
+  L.stage_cap = (k > 0 && n_tiles > 1 && nc <= kMergeStageMax) ? nc : 0;
+  const int a_bytes = bs * 8 + fused_ntr * 8;
+  const int st_bytes = L.stage_cap * 8 + align16(L.stage_cap * 4);
   int o = 0;
-  L.acc = o; L.y = bs * 8; o = align16(bs * 8 + fused_ntr * 8);
+  L.acc = o; L.y = bs * 8; o = align16(a_bytes > st_bytes ? a_bytes : st_bytes);
   L.heard = o; o = align16(o + (bs / 32) * 4);
   L.s_lo = o; o += fused * kThreads * 8;
   L.s_w = o; o += fused * kThreads * 8;
   L.s_pre = o; o = align16(o + (kThreads + 1) * 4);
   L.s_scan = o; o = align16(o + kWaves * 4);
-  L.slot_k = o; o = align16(o + kWaves * C * 8);
-  L.slot_s = o; o = align16(o + kWaves * C * 4);
+  L.slot = o; o = align16(o + kWaves * C * 16);
   L.a_k = o; o = align16(o + L.sel_cap * 8);
   L.a_s = o; o = align16(o + L.sel_cap * 4);
   L.b_k = o; o = align16(o + L.sel_cap * 8);
@@ -193,15 +201,15 @@ constexpr int kMaxE = 4;
 // 4 owns it) -> its k best in (key desc, song asc) order at out[c*k .. c*k+k),
 // missing slots (-1, -1). get(i, key, song) reads candidate i < n; key < 0 =
 // not a candidate. A candidate's slot is its rank = the number of chunk
-// candidates before it in the total order (ranks of distinct songs are distinct).
+// candidates before it in the total order (ranks of distinct songs are
+// distinct). The chunk sits in the wave's LDS slot as 16-byte {key, song}
+// entries read back as broadcast ds_read_b128, 8 in flight per lane.
 template <typename Get>
-__device__ __forceinline__ void select_round(int n, int k, Get get, long long* slot_k, int* slot_s, long long* out_k,
-                                             int* out_s) {
+__device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, long long* out_k, int* out_s) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int E = sel_e(k), C = 64 * E;
   const int nchunks = (n + C - 1) / C;
-  long long* sk = slot_k + w * C;
-  int* ss = slot_s + w * C;
+  int4* sl = slot + w * C;
   for (int c = w; c < nchunks; c += kWaves) {
     const int base = c * C;
     const int cnt = min(C, n - base);
@@ -216,19 +224,28 @@ __device__ __forceinline__ void select_round(int n, int k, Get get, long long* s
         const int j = e * 64 + lane;
         if (j < cnt) get(base + j, key[e], song[e]);
         if (key[e] < 0) { key[e] = kKeyNone; song[e] = INT_MAX; }
-        sk[j] = key[e];
-        ss[j] = song[e];
+        sl[j] = make_int4((int)(unsigned)(key[e] & 0xffffffffll), (int)(key[e] >> 32), song[e], 0);
         nvalid += __popcll(__ballot(key[e] >= 0));
       }
     }
     wave_lds_sync();
     long long* ok = out_k + (size_t)c * k;
     int* os = out_s + (size_t)c * k;
+    const int cnt8 = (cnt + 7) & ~7;  // entries past cnt are (-1, INT_MAX): never before a candidate
 #pragma unroll
     for (int e = 0; e < kMaxE; ++e) {
       if (e < E && key[e] >= 0) {
         int rank = 0;
-        for (int j = 0; j < cnt; ++j) rank += cand_before(sk[j], ss[j], key[e], song[e]) ? 1 : 0;
+        for (int j0 = 0; j0 < cnt8; j0 += 8) {
+          int4 x[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) x[t] = sl[j0 + t];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const long long kx = (long long)(((unsigned long long)(unsigned)x[t].y << 32) | (unsigned)x[t].x);
+            rank += cand_before(kx, x[t].z, key[e], song[e]) ? 1 : 0;
+          }
+        }
         if (rank < k) { ok[rank] = key[e]; os[rank] = song[e]; }
       }
     }
@@ -241,15 +258,15 @@ __device__ __forceinline__ void select_round(int n, int k, Get get, long long* s
 // select_round over the survivors (buffers a/b hold sel_cap entries each).
 // Every thread of the block must call it; it ends with a barrier.
 template <typename Get>
-__device__ __forceinline__ void block_select(int n, int k, Get get, long long* slot_k, int* slot_s, long long* a_k,
-                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s) {
+__device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, long long* a_k, int* a_s,
+                                             long long* b_k, int* b_s, long long* out_k, int* out_s) {
   const int C = 64 * sel_e(k);
   if (n <= C) {
-    select_round(n, k, get, slot_k, slot_s, out_k, out_s);
+    select_round(n, k, get, slot, out_k, out_s);
     __syncthreads();
     return;
   }
-  select_round(n, k, get, slot_k, slot_s, a_k, a_s);
+  select_round(n, k, get, slot, a_k, a_s);
   int m = sel_out(n, k);
   __syncthreads();
   long long* src_k = a_k;
@@ -262,11 +279,11 @@ __device__ __forceinline__ void block_select(int n, int k, Get get, long long* s
       song = src_s[i];
     };
     if (m <= C) {
-      select_round(m, k, from_src, slot_k, slot_s, out_k, out_s);
+      select_round(m, k, from_src, slot, out_k, out_s);
       __syncthreads();
       return;
     }
-    select_round(m, k, from_src, slot_k, slot_s, dst_k, dst_s);
+    select_round(m, k, from_src, slot, dst_k, dst_s);
     m = sel_out(m, k);
     __syncthreads();
     long long* tk = src_k; src_k = dst_k; dst_k = tk;
@@ -334,14 +351,29 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
     s_pre[tid] = pre;
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
-    for (int i = tid; i < total; i += kThreads) {
-      int a = 0, b = n;  // j with s_pre[j] <= i < s_pre[j+1]
-      while (b - a > 1) {
-        const int m = (a + b) >> 1;
-        if (s_pre[m] <= i) a = m; else b = m;
+    // 4 flattened entries per thread in flight: the listener loads of one
+    // batch are issued together, then their LDS atomics.
+    for (int i0 = tid; i0 < total; i0 += 4 * kThreads) {
+      int v[4];
+      unsigned long long wv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r * kThreads;
+        v[r] = -1;
+        wv[r] = 0ull;
+        if (i < total) {
+          int a = 0, b = n;  // j with s_pre[j] <= i < s_pre[j+1]
+          while (b - a > 1) {
+            const int m = (a + b) >> 1;
+            if (s_pre[m] <= i) a = m; else b = m;
+          }
+          v[r] = trs_users[s_lo[a] + (i - s_pre[a])];
+          wv[r] = (unsigned long long)s_w[a];
+        }
       }
-      const int v = trs_users[s_lo[a] + (i - s_pre[a])];
-      atomicAdd(&Y[v], (unsigned long long)s_w[a]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (v[r] >= 0) atomicAdd(&Y[v[r]], wv[r]);
     }
     __syncthreads();
   }
@@ -438,8 +470,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
-  long long* slot_k = reinterpret_cast<long long*>(smem_raw + L.slot_k);
-  int* slot_s = reinterpret_cast<int*>(smem_raw + L.slot_s);
+  int4* slot = reinterpret_cast<int4*>(smem_raw + L.slot);
   long long* a_k = reinterpret_cast<long long*>(smem_raw + L.a_k);
   int* a_s = reinterpret_cast<int*>(smem_raw + L.a_s);
   long long* b_k = reinterpret_cast<long long*>(smem_raw + L.b_k);
@@ -462,6 +493,8 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
   const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  // Prefetch this thread's first epilogue scale (hidden behind stages 1-2).
+  const double sc0 = (MODEL == MR_IBM && tid < bw) ? p.sqrt_c[blo + tid] : 1.0;
 
   if (FUSED) {
     unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
@@ -474,14 +507,33 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
                                  reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi);
     MR_STAMP(1);
     const double rs_u = p.sqrt_te[u];
-    for (int v = tid; v < p.n_tr; v += kThreads) {
-      const unsigned long long y = Y[v];
-      if (y == 0ull) continue;
-      const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
-          y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
-      const int* bp = p.blk_ptr + (size_t)v * stride + tile;
-      const int a = bp[0], b = bp[1];
-      for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+    // 4 neighbours per thread in flight: row-pointer loads, then the first
+    // song of each segment, then the LDS atomics.
+    for (int v0 = tid; v0 < p.n_tr; v0 += 4 * kThreads) {
+      int a[4], b[4], s0[4];
+      unsigned long long y[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int v = v0 + r * kThreads;
+        y[r] = v < p.n_tr ? Y[v] : 0ull;
+        a[r] = b[r] = 0;
+        if (y[r] != 0ull) {
+          const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+          a[r] = bp[0];
+          b[r] = bp[1];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (s0[r] < 0) continue;
+        const int v = v0 + r * kThreads;
+        const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
+            y[r], rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
+        atomicAdd(&acc[s0[r] - blo], q);
+        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+      }
     }
   } else {
     __syncthreads();
@@ -493,12 +545,32 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     const int cnt = p.nbr_cnt[bu];
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-    for (int k = tid; k < cnt; k += kThreads) {
-      const int v = nv[k];
-      const unsigned long long q = (unsigned long long)nq[k];
-      const int* bp = p.blk_ptr + (size_t)v * stride + tile;
-      const int a = bp[0], b = bp[1];
-      for (int x = a; x < b; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+    for (int k0 = tid; k0 < cnt; k0 += 4 * kThreads) {
+      int v[4], a[4], b[4], s0[4];
+      unsigned long long q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + r * kThreads;
+        v[r] = k < cnt ? nv[k] : -1;
+        q[r] = k < cnt ? (unsigned long long)nq[k] : 0ull;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = b[r] = 0;
+        if (v[r] >= 0) {
+          const int* bp = p.blk_ptr + (size_t)v[r] * stride + tile;
+          a[r] = bp[0];
+          b[r] = bp[1];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (s0[r] < 0) continue;
+        atomicAdd(&acc[s0[r] - blo], q[r]);
+        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q[r]);
+      }
     }
   }
   __syncthreads();
@@ -510,7 +582,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   for (int i = tid; i < bw; i += kThreads) {
     const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
     double score = (double)(long long)acc[i] * inv_f;
-    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
+    if (MODEL == MR_IBM) score = score / (i == tid ? sc0 : p.sqrt_c[blo + i]);
     if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
     acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
   }
@@ -526,7 +598,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
+      slot, a_k, a_s, b_k, b_s, fk, fs);
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
@@ -563,14 +635,33 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 #endif
   if (!*flag) return;
 
-  // Last tile of user u: top-k over all tiles' candidates (sc1 loads).
-  block_select(
-      p.n_tiles * k, k,
-      [&](int i, long long& key, int& song) {
-        key = ld_sc1(&ck[i]);
-        song = ld_sc1(&cs[i]);
-      },
-      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
+  // Last tile of user u: top-k over all tiles' candidates (sc1 loads),
+  // staged into LDS region A with all loads in flight at once.
+  const int nc = p.n_tiles * k;
+  if (L.stage_cap >= nc) {
+    long long* mk = reinterpret_cast<long long*>(smem_raw + L.acc);
+    int* ms = reinterpret_cast<int*>(smem_raw + L.acc + L.stage_cap * 8);
+    for (int i = tid; i < nc; i += kThreads) {
+      mk[i] = ld_sc1(&ck[i]);
+      ms[i] = ld_sc1(&cs[i]);
+    }
+    __syncthreads();
+    block_select(
+        nc, k,
+        [&](int i, long long& key, int& song) {
+          key = mk[i];
+          song = ms[i];
+        },
+        slot, a_k, a_s, b_k, b_s, fk, fs);
+  } else {
+    block_select(
+        nc, k,
+        [&](int i, long long& key, int& song) {
+          key = ld_sc1(&ck[i]);
+          song = ld_sc1(&cs[i]);
+        },
+        slot, a_k, a_s, b_k, b_s, fk, fs);
+  }
   for (int r = tid; r < k; r += kThreads) {
     const size_t o = (size_t)u * k + r;
     p.top_key[o] = fk[r];
@@ -598,7 +689,7 @@ struct MergeParams {
 __host__ __device__ inline int merge_lds_bytes(int n, int k) {
   const int C = 64 * sel_e(k);
   const int cap = sel_out(n, k);
-  return align16(kWaves * C * 12) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
+  return align16(kWaves * C * 16) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
 }
 
 __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
@@ -607,9 +698,8 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
   const int n = p.n_lists * p.k_in;
   const int C = 64 * sel_e(k);
   const int cap = sel_out(n, k);
-  long long* slot_k = reinterpret_cast<long long*>(smem_raw);
-  int* slot_s = reinterpret_cast<int*>(slot_k + kWaves * C);
-  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 12));
+  int4* slot = reinterpret_cast<int4*>(smem_raw);
+  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 16));
   int* a_s = reinterpret_cast<int*>(a_k + cap);
   long long* b_k = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(a_k) + align16(cap * 12));
   int* b_s = reinterpret_cast<int*>(b_k + cap);
@@ -626,7 +716,7 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
         key = keys[off];
         song = songs[off];
       },
-      slot_k, slot_s, a_k, a_s, b_k, b_s, fk, fs);
+      slot, a_k, a_s, b_k, b_s, fk, fs);
   const size_t o = (size_t)bu * p.k_out;
   for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
     p.out_keys[o + r] = fk[r];
