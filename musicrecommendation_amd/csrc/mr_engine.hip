@@ -150,9 +150,11 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
 #ifdef MR_STAMPS
 #define MR_STAMP(i)                                                                     \
   do {                                                                                  \
-    if (threadIdx.x == 0 && p.stamps)                                                   \
-      p.stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] =                \
-          (long long)__builtin_amdgcn_s_memrealtime();                                  \
+    if (threadIdx.x == 0 && p.stamps) {                                                 \
+      const size_t sb_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;            \
+      p.stamps[sb_ + (i)] = (long long)__builtin_amdgcn_s_memrealtime();                \
+      p.stamps[sb_ + 8 + (i)] = (long long)__builtin_amdgcn_s_memtime();                \
+    }                                                                                   \
   } while (0)
 #else
 #define MR_STAMP(i) do {} while (0)
@@ -628,8 +630,9 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   MR_STAMP(5);
 #ifdef MR_STAMPS
   if (tid == 0 && p.stamps) {
-    const size_t sb = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+    const size_t sb = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
     p.stamps[sb + 6] = p.stamps[sb + 5];
+    p.stamps[sb + 14] = p.stamps[sb + 13];
     p.stamps[sb + 7] = (long long)(*flag) | ((long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 8);
   }
 #endif
@@ -1044,8 +1047,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->nbr_lds));
   }
 #ifdef MR_STAMPS
-  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * 8))) return rc;
-  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * 8 * 8, st));
+  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * 16))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * 16 * 8, st));
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
@@ -1137,7 +1140,7 @@ int run_model(mr_ctx* c, int model) {
       sp.dense_out = c->dense.p;
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
-      sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * 8 : nullptr;
+      sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * 16 : nullptr;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
     }

@@ -22,10 +22,12 @@ for _ in range(20):
     e.run(model)
 e.sync()
 n = e.n_tiles * ds.n_test
-buf = np.zeros(n * 8, dtype=np.int64)
+buf = np.zeros(n * 16, dtype=np.int64)
 rc = e._L.mr_debug_stamps(e._h, buf.ctypes.data, buf.size)
 assert rc == 0, e._L.mr_last_error()
-st = buf.reshape(n, 8).astype(np.float64)
+full = buf.reshape(n, 16).astype(np.float64)
+st = full[:, :8]
+cyc = full[:, 8:]
 t0 = st[:, 0].min()
 ns = 10.0  # s_memrealtime: 100 MHz
 names = ["start", "stage1", "stage2", "epilogue", "tile-topk", "handoff", "merge(last)"]
@@ -39,5 +41,10 @@ d = (st[last, 6] - st[last, 5]) * ns / 1e3
 print(f"  {'merge(last)':12s} us: med {np.median(d):7.3f}  max {d.max():7.3f}  (n={last.sum()})")
 end = np.where(last, st[:, 6], st[:, 5])
 print("WG end offsets (us): min/med/max", *(np.percentile(end - t0, [0, 50, 100]) * ns / 1e3))
+mhz = (cyc[:, 5] - cyc[:, 0]) / ((st[:, 5] - st[:, 0]) * ns / 1e3)
+print("shader clock during the kernel (MHz): med", np.median(mhz), "min", mhz.min(), "max", mhz.max())
+for i in range(1, 6):
+    d = cyc[:, i] - cyc[:, i - 1]
+    print(f"  {names[i]:12s} kcycles: med {np.median(d) / 1e3:7.2f}")
 xcc = (st[:, 7].astype(np.int64) >> 8) & 15
 print("WGs per XCC:", np.bincount(xcc, minlength=8).tolist())
