@@ -60,11 +60,11 @@ def exchange_topk(songs, keys, group=None):
 
     world = dist.get_world_size(group)
     n_te, k = songs.shape
-    g_songs = torch.empty((world, n_te, k), dtype=songs.dtype, device=songs.device)
-    g_keys = torch.empty((world, n_te, k), dtype=keys.dtype, device=keys.device)
+    g_songs = torch.empty((world * n_te, k), dtype=songs.dtype, device=songs.device)
+    g_keys = torch.empty((world * n_te, k), dtype=keys.dtype, device=keys.device)
     dist.all_gather_into_tensor(g_songs, songs.contiguous(), group=group)
     dist.all_gather_into_tensor(g_keys, keys.contiguous(), group=group)
-    return g_songs, g_keys
+    return g_songs.view(world, n_te, k), g_keys.view(world, n_te, k)
 
 
 def merge_gathered_host(g_songs, g_keys):
