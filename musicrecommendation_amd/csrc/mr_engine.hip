@@ -100,7 +100,8 @@ __host__ __device__ inline int sel_out(int n, int k) {  // survivors of one roun
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot, a_k, a_s, b_k, b_s, fk, fs, flag, sel_cap, stage_cap, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, flag, misc, sel_cap,
+      stage_cap, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -120,7 +121,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   const int nc = n_tiles * kk;
   L.stage_cap = (k > 0 && n_tiles > 1 && nc <= kMergeStageMax) ? nc : 0;
   const int a_bytes = bs * 8 + fused_ntr * 8;
-  const int st_bytes = L.stage_cap * 8 + align16(L.stage_cap * 4);
+  const int st_bytes = 2 * (L.stage_cap * 8 + align16(L.stage_cap * 4));
   int o = 0;
   L.acc = o; L.y = bs * 8; o = align16(a_bytes > st_bytes ? a_bytes : st_bytes);
   L.heard = o; o = align16(o + (bs / 32) * 4);
@@ -129,6 +130,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.s_pre = o; o = align16(o + (kThreads + 1) * 4);
   L.s_scan = o; o = align16(o + kWaves * 4);
   L.slot = o; o = align16(o + kWaves * C * 16);
+  L.slot_hi = o; o = align16(o + kWaves * C * 4);
   L.a_k = o; o = align16(o + L.sel_cap * 8);
   L.a_s = o; o = align16(o + L.sel_cap * 4);
   L.b_k = o; o = align16(o + L.sel_cap * 8);
@@ -136,6 +138,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.fk = o; o = align16(o + kMaxTopK * 8);
   L.fs = o; o = align16(o + kMaxTopK * 4);
   L.flag = o; o = align16(o + 4);
+  L.misc = o; o = align16(o + 16);
   L.total = o;
   return L;
 }
@@ -203,50 +206,88 @@ constexpr int kMaxE = 4;
 // 4 owns it) -> its k best in (key desc, song asc) order at out[c*k .. c*k+k),
 // missing slots (-1, -1). get(i, key, song) reads candidate i < n; key < 0 =
 // not a candidate. A candidate's slot is its rank = the number of chunk
-// candidates before it in the total order (ranks of distinct songs are
-// distinct). The chunk sits in the wave's LDS slot as 16-byte {key, song}
-// entries read back as broadcast ds_read_b128, 8 in flight per lane.
+// candidates before it in the total order (ranks of distinct songs are distinct).
+//  1. coarse: every lane counts the chunk's candidates whose high key word is
+//     strictly greater than its own (32-bit compares over broadcast reads);
+//     >= k of them means the candidate is out;
+//  2. exact: survivors (all candidates before any survivor are survivors too)
+//     are compacted into the wave's slot and ranked on (key, song).
 template <typename Get>
-__device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, long long* out_k, int* out_s) {
+__device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, int* slot_hi, long long* out_k,
+                                             int* out_s) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int E = sel_e(k), C = 64 * E;
   const int nchunks = (n + C - 1) / C;
   int4* sl = slot + w * C;
+  int* sh = slot_hi + w * C;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int c = w; c < nchunks; c += kWaves) {
     const int base = c * C;
     const int cnt = min(C, n - base);
     long long key[kMaxE];
     int song[kMaxE];
+    int hi[kMaxE];
     int nvalid = 0;
 #pragma unroll
     for (int e = 0; e < kMaxE; ++e) {
       key[e] = kKeyNone;
       song[e] = INT_MAX;
+      hi[e] = -1;
       if (e < E) {
         const int j = e * 64 + lane;
         if (j < cnt) get(base + j, key[e], song[e]);
         if (key[e] < 0) { key[e] = kKeyNone; song[e] = INT_MAX; }
-        sl[j] = make_int4((int)(unsigned)(key[e] & 0xffffffffll), (int)(key[e] >> 32), song[e], 0);
+        hi[e] = (int)(key[e] >> 32);  // -1 for "no candidate": below every valid word
+        sh[j] = hi[e];
         nvalid += __popcll(__ballot(key[e] >= 0));
+      }
+    }
+    wave_lds_sync();
+    // 1. coarse counts, 4 words per broadcast ds_read_b128
+    int gt[kMaxE];
+#pragma unroll
+    for (int e = 0; e < kMaxE; ++e) gt[e] = 0;
+    const int4* sh4 = reinterpret_cast<const int4*>(sh);
+    for (int j4 = 0; j4 < C / 4; j4 += 4) {
+      int4 x[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) x[t] = sh4[j4 + t];
+#pragma unroll
+      for (int e = 0; e < kMaxE; ++e) {
+        if (e < E) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            gt[e] += (x[t].x > hi[e]) + (x[t].y > hi[e]) + (x[t].z > hi[e]) + (x[t].w > hi[e]);
+        }
+      }
+    }
+    // 2. compact the survivors into the slot (wave-local positions by ballot)
+    bool keep[kMaxE];
+    int m = 0;
+#pragma unroll
+    for (int e = 0; e < kMaxE; ++e) {
+      keep[e] = false;
+      if (e < E) {
+        keep[e] = key[e] >= 0 && gt[e] < k;
+        const unsigned long long bal = __ballot(keep[e]);
+        if (keep[e]) {
+          const int pos = m + __popcll(bal & lt_mask);
+          sl[pos] = make_int4((int)(unsigned)(key[e] & 0xffffffffll), (int)(key[e] >> 32), song[e], 0);
+        }
+        m += __popcll(bal);
       }
     }
     wave_lds_sync();
     long long* ok = out_k + (size_t)c * k;
     int* os = out_s + (size_t)c * k;
-    const int cnt8 = (cnt + 7) & ~7;  // entries past cnt are (-1, INT_MAX): never before a candidate
 #pragma unroll
     for (int e = 0; e < kMaxE; ++e) {
-      if (e < E && key[e] >= 0) {
+      if (keep[e]) {
         int rank = 0;
-        for (int j0 = 0; j0 < cnt8; j0 += 8) {
-          int4 x[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) x[t] = sl[j0 + t];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const long long kx = (long long)(((unsigned long long)(unsigned)x[t].y << 32) | (unsigned)x[t].x);
-            rank += cand_before(kx, x[t].z, key[e], song[e]) ? 1 : 0;
-          }
+        for (int j = 0; j < m; ++j) {
+          const int4 x = sl[j];
+          const long long kx = (long long)(((unsigned long long)(unsigned)x.y << 32) | (unsigned)x.x);
+          rank += cand_before(kx, x.z, key[e], song[e]) ? 1 : 0;
         }
         if (rank < k) { ok[rank] = key[e]; os[rank] = song[e]; }
       }
@@ -260,15 +301,15 @@ __device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, 
 // select_round over the survivors (buffers a/b hold sel_cap entries each).
 // Every thread of the block must call it; it ends with a barrier.
 template <typename Get>
-__device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, long long* a_k, int* a_s,
-                                             long long* b_k, int* b_s, long long* out_k, int* out_s) {
+__device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, int* slot_hi, long long* a_k,
+                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s) {
   const int C = 64 * sel_e(k);
   if (n <= C) {
-    select_round(n, k, get, slot, out_k, out_s);
+    select_round(n, k, get, slot, slot_hi, out_k, out_s);
     __syncthreads();
     return;
   }
-  select_round(n, k, get, slot, a_k, a_s);
+  select_round(n, k, get, slot, slot_hi, a_k, a_s);
   int m = sel_out(n, k);
   __syncthreads();
   long long* src_k = a_k;
@@ -281,11 +322,11 @@ __device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, 
       song = src_s[i];
     };
     if (m <= C) {
-      select_round(m, k, from_src, slot, out_k, out_s);
+      select_round(m, k, from_src, slot, slot_hi, out_k, out_s);
       __syncthreads();
       return;
     }
-    select_round(m, k, from_src, slot, dst_k, dst_s);
+    select_round(m, k, from_src, slot, slot_hi, dst_k, dst_s);
     m = sel_out(m, k);
     __syncthreads();
     long long* tk = src_k; src_k = dst_k; dst_k = tk;
@@ -353,13 +394,13 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
     s_pre[tid] = pre;
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
-    // 4 flattened entries per thread in flight: the listener loads of one
+    // 8 flattened entries per thread in flight: the listener loads of one
     // batch are issued together, then their LDS atomics.
-    for (int i0 = tid; i0 < total; i0 += 4 * kThreads) {
-      int v[4];
-      unsigned long long wv[4];
+    for (int i0 = tid; i0 < total; i0 += 8 * kThreads) {
+      int v[8];
+      unsigned long long wv[8];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 8; ++r) {
         const int i = i0 + r * kThreads;
         v[r] = -1;
         wv[r] = 0ull;
@@ -374,7 +415,7 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 8; ++r)
         if (v[r] >= 0) atomicAdd(&Y[v[r]], wv[r]);
     }
     __syncthreads();
@@ -473,6 +514,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
   int4* slot = reinterpret_cast<int4*>(smem_raw + L.slot);
+  int* slot_hi = reinterpret_cast<int*>(smem_raw + L.slot_hi);
   long long* a_k = reinterpret_cast<long long*>(smem_raw + L.a_k);
   int* a_s = reinterpret_cast<int*>(smem_raw + L.a_s);
   long long* b_k = reinterpret_cast<long long*>(smem_raw + L.b_k);
@@ -499,6 +541,19 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const double sc0 = (MODEL == MR_IBM && tid < bw) ? p.sqrt_c[blo + tid] : 1.0;
 
   if (FUSED) {
+    // The tile's row pointers do not depend on the test user: issue them now,
+    // they land while stage 1 runs (train users tid + 256 r, r < 4).
+    int pa[4], pb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = tid + r * kThreads;
+      pa[r] = pb[r] = 0;
+      if (v < p.n_tr) {
+        const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+        pa[r] = bp[0];
+        pb[r] = bp[1];
+      }
+    }
     unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
     for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
     __syncthreads();
@@ -520,9 +575,14 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         y[r] = v < p.n_tr ? Y[v] : 0ull;
         a[r] = b[r] = 0;
         if (y[r] != 0ull) {
-          const int* bp = p.blk_ptr + (size_t)v * stride + tile;
-          a[r] = bp[0];
-          b[r] = bp[1];
+          if (v0 == tid) {  // first pass: prefetched
+            a[r] = pa[r];
+            b[r] = pb[r];
+          } else {
+            const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+            a[r] = bp[0];
+            b[r] = bp[1];
+          }
         }
       }
 #pragma unroll
@@ -600,7 +660,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      slot, a_k, a_s, b_k, b_s, fk, fs);
+      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
@@ -642,20 +702,42 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   // staged into LDS region A with all loads in flight at once.
   const int nc = p.n_tiles * k;
   if (L.stage_cap >= nc) {
+    // Stage the candidates (one batch of sc1 loads) and the bound
+    // B = max over tiles of their k-th key: every tile holds k candidates
+    // >= its k-th key, so the user's k-th best is >= B and candidates below
+    // B are out. Survivors are compacted (order is irrelevant: ranks are exact).
+    const int scap = L.stage_cap;
     long long* mk = reinterpret_cast<long long*>(smem_raw + L.acc);
-    int* ms = reinterpret_cast<int*>(smem_raw + L.acc + L.stage_cap * 8);
+    int* ms = reinterpret_cast<int*>(smem_raw + L.acc + scap * 8);
+    long long* vk = reinterpret_cast<long long*>(smem_raw + L.acc + scap * 8 + align16(scap * 4));
+    int* vs = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(vk) + scap * 8);
+    unsigned long long* sbound = reinterpret_cast<unsigned long long*>(smem_raw + L.misc);
+    int* scount = reinterpret_cast<int*>(smem_raw + L.misc + 8);
+    if (tid == 0) { *sbound = 0ull; *scount = 0; }
+    __syncthreads();
     for (int i = tid; i < nc; i += kThreads) {
-      mk[i] = ld_sc1(&ck[i]);
+      const long long key = ld_sc1(&ck[i]);
+      mk[i] = key;
       ms[i] = ld_sc1(&cs[i]);
+      if ((i % k) == k - 1 && key >= 0) atomicMax(sbound, (unsigned long long)key);
+    }
+    __syncthreads();
+    const long long bound = (long long)*sbound;
+    for (int i = tid; i < nc; i += kThreads) {
+      if (mk[i] >= 0 && mk[i] >= bound) {
+        const int pos = atomicAdd(scount, 1);
+        vk[pos] = mk[i];
+        vs[pos] = ms[i];
+      }
     }
     __syncthreads();
     block_select(
-        nc, k,
+        *scount, k,
         [&](int i, long long& key, int& song) {
-          key = mk[i];
-          song = ms[i];
+          key = vk[i];
+          song = vs[i];
         },
-        slot, a_k, a_s, b_k, b_s, fk, fs);
+        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
   } else {
     block_select(
         nc, k,
@@ -663,7 +745,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
           key = ld_sc1(&ck[i]);
           song = ld_sc1(&cs[i]);
         },
-        slot, a_k, a_s, b_k, b_s, fk, fs);
+        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
   }
   for (int r = tid; r < k; r += kThreads) {
     const size_t o = (size_t)u * k + r;
@@ -692,7 +774,7 @@ struct MergeParams {
 __host__ __device__ inline int merge_lds_bytes(int n, int k) {
   const int C = 64 * sel_e(k);
   const int cap = sel_out(n, k);
-  return align16(kWaves * C * 16) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
+  return align16(kWaves * C * 20) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
 }
 
 __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
@@ -702,7 +784,8 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
   const int C = 64 * sel_e(k);
   const int cap = sel_out(n, k);
   int4* slot = reinterpret_cast<int4*>(smem_raw);
-  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 16));
+  int* slot_hi = reinterpret_cast<int*>(smem_raw + kWaves * C * 16);
+  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 20));
   int* a_s = reinterpret_cast<int*>(a_k + cap);
   long long* b_k = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(a_k) + align16(cap * 12));
   int* b_s = reinterpret_cast<int*>(b_k + cap);
@@ -719,7 +802,7 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
         key = keys[off];
         song = songs[off];
       },
-      slot, a_k, a_s, b_k, b_s, fk, fs);
+      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
   const size_t o = (size_t)bu * p.k_out;
   for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
     p.out_keys[o + r] = fk[r];
