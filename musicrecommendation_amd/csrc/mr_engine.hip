@@ -150,15 +150,17 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
 // Diagnostic build only (-DMR_STAMPS, libmr_engine_stamps.so): thread 0 of
 // each scoring workgroup records s_memrealtime (100 MHz) at phase boundaries
 // into a debug buffer; the production build compiles these away.
+constexpr int kStampSlots = 32;  // [0,16): s_memrealtime, [16,32): s_memtime
+__device__ __forceinline__ void stamp_at(long long* sb, int i) {
 #ifdef MR_STAMPS
-#define MR_STAMP(i)                                                                     \
-  do {                                                                                  \
-    if (threadIdx.x == 0 && p.stamps) {                                                 \
-      const size_t sb_ = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;            \
-      p.stamps[sb_ + (i)] = (long long)__builtin_amdgcn_s_memrealtime();                \
-      p.stamps[sb_ + 8 + (i)] = (long long)__builtin_amdgcn_s_memtime();                \
-    }                                                                                   \
-  } while (0)
+  if (sb && threadIdx.x == 0) {
+    sb[i] = (long long)__builtin_amdgcn_s_memrealtime();
+    sb[16 + i] = (long long)__builtin_amdgcn_s_memtime();
+  }
+#endif
+}
+#ifdef MR_STAMPS
+#define MR_STAMP(i) stamp_at(p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr, (i))
 #else
 #define MR_STAMP(i) do {} while (0)
 #endif
@@ -302,16 +304,19 @@ __device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, 
 // Every thread of the block must call it; it ends with a barrier.
 template <typename Get>
 __device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, int* slot_hi, long long* a_k,
-                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s) {
+                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s,
+                                             long long* sb = nullptr, int round0_slot = 0) {
   const int C = 64 * sel_e(k);
   if (n <= C) {
     select_round(n, k, get, slot, slot_hi, out_k, out_s);
     __syncthreads();
+    stamp_at(sb, round0_slot);
     return;
   }
   select_round(n, k, get, slot, slot_hi, a_k, a_s);
   int m = sel_out(n, k);
   __syncthreads();
+  stamp_at(sb, round0_slot);
   long long* src_k = a_k;
   int* src_s = a_s;
   long long* dst_k = b_k;
@@ -532,6 +537,11 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const int bw = bhi - blo;
   const int stride = p.n_tiles + 1;
   const double two_f = ldexp(1.0, p.frac_bits);
+#ifdef MR_STAMPS
+  long long* sb = p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr;
+#else
+  long long* sb = nullptr;
+#endif
   MR_STAMP(0);
 
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
@@ -660,7 +670,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
+      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, sb, 10);
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
@@ -689,12 +699,8 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   __syncthreads();
   MR_STAMP(5);
 #ifdef MR_STAMPS
-  if (tid == 0 && p.stamps) {
-    const size_t sb = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
-    p.stamps[sb + 6] = p.stamps[sb + 5];
-    p.stamps[sb + 14] = p.stamps[sb + 13];
-    p.stamps[sb + 7] = (long long)(*flag) | ((long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 8);
-  }
+  if (tid == 0 && sb)
+    sb[15] = (long long)(*flag) | ((long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 8);
 #endif
   if (!*flag) return;
 
@@ -722,6 +728,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       if ((i % k) == k - 1 && key >= 0) atomicMax(sbound, (unsigned long long)key);
     }
     __syncthreads();
+    MR_STAMP(6);
     const long long bound = (long long)*sbound;
     for (int i = tid; i < nc; i += kThreads) {
       if (mk[i] >= 0 && mk[i] >= bound) {
@@ -731,13 +738,15 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       }
     }
     __syncthreads();
+    MR_STAMP(7);
     block_select(
         *scount, k,
         [&](int i, long long& key, int& song) {
           key = vk[i];
           song = vs[i];
         },
-        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
+        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, sb, 11);
+    MR_STAMP(8);
   } else {
     block_select(
         nc, k,
@@ -754,7 +763,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
   }
   if (tid == 0) p.counter[u] = 0u;  // ready for the next launch (kernel boundary orders it)
-  MR_STAMP(6);
+  MR_STAMP(9);
 }
 
 // ---------------------------------------------------------------------------
@@ -1130,8 +1139,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->nbr_lds));
   }
 #ifdef MR_STAMPS
-  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * 16))) return rc;
-  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * 16 * 8, st));
+  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * kStampSlots))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * kStampSlots * 8, st));
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
@@ -1223,7 +1232,7 @@ int run_model(mr_ctx* c, int model) {
       sp.dense_out = c->dense.p;
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
-      sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * 16 : nullptr;
+      sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
     }

@@ -1,4 +1,4 @@
-"""Phase timestamps of the scoring kernel (diagnostic build).
+"""Phase timestamps of the scoring kernel (diagnostic build libmr_engine_stamps.so).
 Usage: python scripts/stamps.py [config] [model] [block_songs] [stage1]"""
 import os
 import sys
@@ -22,29 +22,40 @@ for _ in range(20):
     e.run(model)
 e.sync()
 n = e.n_tiles * ds.n_test
-buf = np.zeros(n * 16, dtype=np.int64)
+buf = np.zeros(n * 32, dtype=np.int64)
 rc = e._L.mr_debug_stamps(e._h, buf.ctypes.data, buf.size)
 assert rc == 0, e._L.mr_last_error()
-full = buf.reshape(n, 16).astype(np.float64)
-st = full[:, :8]
-cyc = full[:, 8:]
-t0 = st[:, 0].min()
-ns = 10.0  # s_memrealtime: 100 MHz
-names = ["start", "stage1", "stage2", "epilogue", "tile-topk", "handoff", "merge(last)"]
+full = buf.reshape(n, 32)
+rt = full[:, :16].astype(np.float64) * 10.0 / 1e3  # us (100 MHz)
+cy = full[:, 16:].astype(np.float64)
+last = (full[:, 15] & 1) == 1
+t0 = rt[:, 0].min()
 print(f"{cfg} {model} fused={e.fused} bs={e.block_songs} tiles={e.n_tiles} WGs={n}")
-print("WG start offsets (us): min/med/max", *(np.percentile(st[:, 0] - t0, [0, 50, 100]) * ns / 1e3))
-for i in range(1, 6):
-    d = (st[:, i] - st[:, i - 1]) * ns / 1e3
-    print(f"  {names[i]:12s} us: med {np.median(d):7.3f}  p90 {np.percentile(d, 90):7.3f}  max {d.max():7.3f}")
-last = (st[:, 7].astype(np.int64) & 1) == 1
-d = (st[last, 6] - st[last, 5]) * ns / 1e3
-print(f"  {'merge(last)':12s} us: med {np.median(d):7.3f}  max {d.max():7.3f}  (n={last.sum()})")
-end = np.where(last, st[:, 6], st[:, 5])
-print("WG end offsets (us): min/med/max", *(np.percentile(end - t0, [0, 50, 100]) * ns / 1e3))
-mhz = (cyc[:, 5] - cyc[:, 0]) / ((st[:, 5] - st[:, 0]) * ns / 1e3)
-print("shader clock during the kernel (MHz): med", np.median(mhz), "min", mhz.min(), "max", mhz.max())
-for i in range(1, 6):
-    d = cyc[:, i] - cyc[:, i - 1]
-    print(f"  {names[i]:12s} kcycles: med {np.median(d) / 1e3:7.2f}")
-xcc = (st[:, 7].astype(np.int64) >> 8) & 15
-print("WGs per XCC:", np.bincount(xcc, minlength=8).tolist())
+mhz = (cy[:, 5] - cy[:, 0]) / (rt[:, 5] - rt[:, 0])
+print(f"clock MHz med {np.median(mhz):.0f}; WG start offsets us min/med/max",
+      *np.round(np.percentile(rt[:, 0] - t0, [0, 50, 100]), 2))
+
+
+def phase(name, a, b, rows=None):
+    rows = np.ones(n, bool) if rows is None else rows
+    d = rt[rows, b] - rt[rows, a]
+    c = cy[rows, b] - cy[rows, a]
+    print(f"  {name:22s} us med {np.median(d):7.3f} p90 {np.percentile(d, 90):7.3f} max {d.max():7.3f}"
+          f"   kcyc med {np.median(c) / 1e3:6.2f}")
+
+
+phase("stage1", 0, 1)
+phase("stage2", 1, 2)
+phase("epilogue", 2, 3)
+phase("tile-topk round0", 3, 10)
+phase("tile-topk final", 10, 4)
+phase("handoff", 4, 5)
+phase("merge stage", 5, 6, last)
+phase("merge compact", 6, 7, last)
+phase("merge select r0", 7, 11, last)
+phase("merge select fin", 11, 8, last)
+phase("merge write", 8, 9, last)
+end = np.where(last, rt[:, 9], rt[:, 5])
+print("WG end offsets (us) min/med/max", *np.round(np.percentile(end - t0, [0, 50, 100]), 2))
+lu = np.where(last)[0]
+print("last-WG merge start (us) per user:", np.round(rt[lu, 5] - t0, 2).tolist())
