@@ -46,6 +46,7 @@ constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS 
 constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64)
 constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live together
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
+constexpr int kMaxTopkTile = 1024;        // songs per tile when the top-k is on
 
 thread_local std::string g_err = "no error";
 
@@ -85,43 +86,26 @@ namespace {
   } while (0)
 
 // ---------------------------------------------------------------------------
-// Top-k selection geometry. A wave ranks a chunk of C = 64*E candidates by
-// counting (every lane compares its candidates with all C, broadcast LDS
-// reads, no dependent shuffle chains) and keeps the chunk's k best; rounds
-// repeat over the survivors until one chunk is left. C must exceed k.
-// ---------------------------------------------------------------------------
-__host__ __device__ inline int sel_e(int k) { return k <= 16 ? 1 : (k <= 32 ? 2 : 4); }
-__host__ __device__ inline int sel_out(int n, int k) {  // survivors of one round over n candidates
-  const int c = 64 * sel_e(k);
-  return ((n + c - 1) / c) * k;
-}
-
-// ---------------------------------------------------------------------------
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, flag, misc, sel_cap,
-      stage_cap, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, stage_lists, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ inline int merge_lists_per_pass(int k);
 
-constexpr int kMergeStageMax = 2048;  // tile candidates staged in LDS for the in-launch merge
-
-// Region A (offset 0) first holds the tile accumulators (+ the fused path's
-// neighbour array Y); once the tile's own top-k is out it is reused to stage
-// the user's tile candidates for the merge (stage_cap entries: keys, songs).
+// Region A (offset 0) holds the tile accumulators (+ the fused path's
+// neighbour array Y); after the tile's own top-k it is reused to stage tile
+// candidate lists for the in-launch merge (stage_lists lists per pass).
 __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles) {
   ScoreLds L;
   const int fused = fused_ntr > 0 ? 1 : 0;
   const int kk = k > 0 ? k : 1;
-  const int C = 64 * sel_e(kk);
-  const int out_tile = sel_out(bs, kk), out_merge = sel_out(n_tiles * kk, kk);
-  L.sel_cap = out_tile > out_merge ? out_tile : out_merge;
-  const int nc = n_tiles * kk;
-  L.stage_cap = (k > 0 && n_tiles > 1 && nc <= kMergeStageMax) ? nc : 0;
+  const int per = merge_lists_per_pass(kk);
+  L.stage_lists = (k > 0 && n_tiles > 1) ? (n_tiles < per ? n_tiles : per) : 0;
   const int a_bytes = bs * 8 + fused_ntr * 8;
-  const int st_bytes = 2 * (L.stage_cap * 8 + align16(L.stage_cap * 4));
+  const int st_bytes = L.stage_lists * kk * 8 + align16(L.stage_lists * kk * 4);
   int o = 0;
   L.acc = o; L.y = bs * 8; o = align16(a_bytes > st_bytes ? a_bytes : st_bytes);
   L.heard = o; o = align16(o + (bs / 32) * 4);
@@ -129,16 +113,11 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.s_w = o; o += fused * kThreads * 8;
   L.s_pre = o; o = align16(o + (kThreads + 1) * 4);
   L.s_scan = o; o = align16(o + kWaves * 4);
-  L.slot = o; o = align16(o + kWaves * C * 16);
-  L.slot_hi = o; o = align16(o + kWaves * C * 4);
-  L.a_k = o; o = align16(o + L.sel_cap * 8);
-  L.a_s = o; o = align16(o + L.sel_cap * 4);
-  L.b_k = o; o = align16(o + L.sel_cap * 8);
-  L.b_s = o; o = align16(o + L.sel_cap * 4);
+  L.wk = o; o = align16(o + kWaves * kMaxTopK * 8);
+  L.ws = o; o = align16(o + kWaves * kMaxTopK * 4);
   L.fk = o; o = align16(o + kMaxTopK * 8);
   L.fs = o; o = align16(o + kMaxTopK * 4);
-  L.flag = o; o = align16(o + 4);
-  L.misc = o; o = align16(o + 16);
+  L.flag = o; o = align16(o + 16);
   L.total = o;
   return L;
 }
@@ -193,150 +172,149 @@ __device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, 
   return ka > kb || (ka == kb && sa < sb);
 }
 
-// Make a wave's LDS writes visible to the other lanes of the same wave (LDS
-// operations of one wave complete in order; the fences stop the compiler
-// from moving the accesses across).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// ---------------------------------------------------------------------------
+// Top-k selection, all in registers + DPP (no LDS round trips on the chain).
+// ---------------------------------------------------------------------------
+
+// One step of a wave argmax: take the better of my candidate and the one the
+// DPP pattern CTRL routes to me (invalid sources keep my own: idempotent).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void argmax_step(long long& k, int& s) {
+  const int lo = (int)(unsigned)(k & 0xffffffffll), hi = (int)(k >> 32);
+  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false);
+  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false);
+  const int s2 = __builtin_amdgcn_update_dpp(s, s, CTRL, ROW_MASK, 0xf, false);
+  const long long k2 = (long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2);
+  if (cand_before(k2, s2, k, s)) { k = k2; s = s2; }
 }
 
-constexpr int kMaxE = 4;
-
-// One selection round: chunk c of C = 64*E consecutive candidates (wave c mod
-// 4 owns it) -> its k best in (key desc, song asc) order at out[c*k .. c*k+k),
-// missing slots (-1, -1). get(i, key, song) reads candidate i < n; key < 0 =
-// not a candidate. A candidate's slot is its rank = the number of chunk
-// candidates before it in the total order (ranks of distinct songs are distinct).
-//  1. coarse: every lane counts the chunk's candidates whose high key word is
-//     strictly greater than its own (32-bit compares over broadcast reads);
-//     >= k of them means the candidate is out;
-//  2. exact: survivors (all candidates before any survivor are survivors too)
-//     are compacted into the wave's slot and ranked on (key, song).
-template <typename Get>
-__device__ __forceinline__ void select_round(int n, int k, Get get, int4* slot, int* slot_hi, long long* out_k,
-                                             int* out_s) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int E = sel_e(k), C = 64 * E;
-  const int nchunks = (n + C - 1) / C;
-  int4* sl = slot + w * C;
-  int* sh = slot_hi + w * C;
-  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int c = w; c < nchunks; c += kWaves) {
-    const int base = c * C;
-    const int cnt = min(C, n - base);
-    long long key[kMaxE];
-    int song[kMaxE];
-    int hi[kMaxE];
-    int nvalid = 0;
-#pragma unroll
-    for (int e = 0; e < kMaxE; ++e) {
-      key[e] = kKeyNone;
-      song[e] = INT_MAX;
-      hi[e] = -1;
-      if (e < E) {
-        const int j = e * 64 + lane;
-        if (j < cnt) get(base + j, key[e], song[e]);
-        if (key[e] < 0) { key[e] = kKeyNone; song[e] = INT_MAX; }
-        hi[e] = (int)(key[e] >> 32);  // -1 for "no candidate": below every valid word
-        sh[j] = hi[e];
-        nvalid += __popcll(__ballot(key[e] >= 0));
-      }
-    }
-    wave_lds_sync();
-    // 1. coarse counts, 4 words per broadcast ds_read_b128
-    int gt[kMaxE];
-#pragma unroll
-    for (int e = 0; e < kMaxE; ++e) gt[e] = 0;
-    const int4* sh4 = reinterpret_cast<const int4*>(sh);
-    for (int j4 = 0; j4 < C / 4; j4 += 4) {
-      int4 x[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) x[t] = sh4[j4 + t];
-#pragma unroll
-      for (int e = 0; e < kMaxE; ++e) {
-        if (e < E) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            gt[e] += (x[t].x > hi[e]) + (x[t].y > hi[e]) + (x[t].z > hi[e]) + (x[t].w > hi[e]);
-        }
-      }
-    }
-    // 2. compact the survivors into the slot (wave-local positions by ballot)
-    bool keep[kMaxE];
-    int m = 0;
-#pragma unroll
-    for (int e = 0; e < kMaxE; ++e) {
-      keep[e] = false;
-      if (e < E) {
-        keep[e] = key[e] >= 0 && gt[e] < k;
-        const unsigned long long bal = __ballot(keep[e]);
-        if (keep[e]) {
-          const int pos = m + __popcll(bal & lt_mask);
-          sl[pos] = make_int4((int)(unsigned)(key[e] & 0xffffffffll), (int)(key[e] >> 32), song[e], 0);
-        }
-        m += __popcll(bal);
-      }
-    }
-    wave_lds_sync();
-    long long* ok = out_k + (size_t)c * k;
-    int* os = out_s + (size_t)c * k;
-#pragma unroll
-    for (int e = 0; e < kMaxE; ++e) {
-      if (keep[e]) {
-        int rank = 0;
-        for (int j = 0; j < m; ++j) {
-          const int4 x = sl[j];
-          const long long kx = (long long)(((unsigned long long)(unsigned)x.y << 32) | (unsigned)x.x);
-          rank += cand_before(kx, x.z, key[e], song[e]) ? 1 : 0;
-        }
-        if (rank < k) { ok[rank] = key[e]; os[rank] = song[e]; }
-      }
-    }
-    for (int r = nvalid + lane; r < k; r += 64) { ok[r] = kKeyNone; os[r] = -1; }
-    wave_lds_sync();  // the slot is rewritten by the wave's next chunk
-  }
+// Wave-wide best candidate, returned (wave-uniform) to every lane:
+// row_shr 1/2/4/8 leave each row's best in its lane 15, row_bcast 15/31
+// carry the rows into lane 63, readlane broadcasts it.
+__device__ __forceinline__ void wave_argmax(long long& k, int& s) {
+  argmax_step<0x111, 0xf>(k, s);  // row_shr:1
+  argmax_step<0x112, 0xf>(k, s);  // row_shr:2
+  argmax_step<0x114, 0xf>(k, s);  // row_shr:4
+  argmax_step<0x118, 0xf>(k, s);  // row_shr:8
+  argmax_step<0x142, 0xa>(k, s);  // row_bcast:15 -> rows 1, 3
+  argmax_step<0x143, 0xc>(k, s);  // row_bcast:31 -> rows 2, 3
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)(k & 0xffffffffll), 63);
+  const int hi = __builtin_amdgcn_readlane((int)(k >> 32), 63);
+  s = __builtin_amdgcn_readlane(s, 63);
+  k = (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// Block top-k of n candidates -> out_k/out_s[0..k) (LDS), sorted; rounds of
-// select_round over the survivors (buffers a/b hold sel_cap entries each).
-// Every thread of the block must call it; it ends with a barrier.
+constexpr int kRegCand = 4;  // candidates per lane kept in registers
+
+// A wave's top-k: round r takes the best candidate strictly after round
+// r-1's winner in the total order (candidates are distinct songs, so no
+// "taken" marks). Lane l supplies m <= kRegCand candidates via get(j, ...),
+// loaded once into registers; key < 0 = no candidate. Lane 0 writes the
+// sorted list to out_k/out_s[0..k); missing slots (-1, -1).
 template <typename Get>
-__device__ __forceinline__ void block_select(int n, int k, Get get, int4* slot, int* slot_hi, long long* a_k,
-                                             int* a_s, long long* b_k, int* b_s, long long* out_k, int* out_s,
-                                             long long* sb = nullptr, int round0_slot = 0) {
-  const int C = 64 * sel_e(k);
-  if (n <= C) {
-    select_round(n, k, get, slot, slot_hi, out_k, out_s);
-    __syncthreads();
-    stamp_at(sb, round0_slot);
-    return;
+__device__ __forceinline__ void wave_topk(int m, Get get, int k, long long* out_k, int* out_s) {
+  const int lane = threadIdx.x & 63;
+  long long rk[kRegCand];
+  int rs[kRegCand];
+#pragma unroll
+  for (int j = 0; j < kRegCand; ++j) {
+    rk[j] = kKeyNone;
+    rs[j] = INT_MAX;
+    if (j < m) get(j, rk[j], rs[j]);
+    if (rk[j] < 0) { rk[j] = kKeyNone; rs[j] = INT_MAX; }
   }
-  select_round(n, k, get, slot, slot_hi, a_k, a_s);
-  int m = sel_out(n, k);
+  long long pk = LLONG_MAX;
+  int ps = -1;
+  int r = 0;
+  for (; r < k; ++r) {
+    long long bk = kKeyNone;
+    int bs = INT_MAX;
+#pragma unroll
+    for (int j = 0; j < kRegCand; ++j)
+      if (rk[j] >= 0 && cand_before(pk, ps, rk[j], rs[j]) && cand_before(rk[j], rs[j], bk, bs)) {
+        bk = rk[j];
+        bs = rs[j];
+      }
+    wave_argmax(bk, bs);
+    if (bk < 0) break;  // wave-uniform
+    if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
+    pk = bk;
+    ps = bs;
+  }
+  for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
+}
+
+// Tournament over L sorted lists (desc, (-1,-1)-padded) of length k in LDS,
+// run by ONE wave: lane l owns lists l, l+64, l+128, l+192 and their heads;
+// each round the wave argmax of the heads is the next winner and its owner
+// advances that list. Lane 0 writes the merged top-k to out_k/out_s.
+__device__ __forceinline__ void wave_merge_lists(int L, int k, const long long* lk, const int* ls,
+                                                 long long* out_k, int* out_s) {
+  const int lane = threadIdx.x & 63;
+  int pos[4];
+  long long hk[4];
+  int hs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int l = lane + 64 * j;
+    pos[j] = 0;
+    hk[j] = kKeyNone;
+    hs[j] = INT_MAX;
+    if (l < L) {
+      hk[j] = lk[(size_t)l * k];
+      hs[j] = ls[(size_t)l * k];
+      if (hk[j] < 0) { hk[j] = kKeyNone; hs[j] = INT_MAX; }
+    }
+  }
+  int r = 0;
+  for (; r < k; ++r) {
+    long long bk = kKeyNone;
+    int bs = INT_MAX;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cand_before(hk[j], hs[j], bk, bs)) { bk = hk[j]; bs = hs[j]; }
+    wave_argmax(bk, bs);
+    if (bk < 0) break;  // wave-uniform
+    if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (hk[j] == bk && hs[j] == bs) {  // songs are unique: exactly one owner
+        const int l = lane + 64 * j;
+        ++pos[j];
+        hk[j] = kKeyNone;
+        hs[j] = INT_MAX;
+        if (pos[j] < k) {
+          hk[j] = lk[(size_t)l * k + pos[j]];
+          hs[j] = ls[(size_t)l * k + pos[j]];
+          if (hk[j] < 0) { hk[j] = kKeyNone; hs[j] = INT_MAX; }
+        }
+      }
+    }
+  }
+  for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
+}
+
+// Block top-k of n <= 4 * 256 candidates get(i) into out (LDS): every wave
+// selects from its elements i = w*64 + lane + 256 j, then wave 0 merges the
+// four sorted wave lists. All threads call it; it ends with a barrier.
+template <typename Get>
+__device__ __forceinline__ void block_topk(int n, int k, Get get, long long* wk, int* ws, long long* out_k,
+                                           int* out_s) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int first = w * 64 + lane;
+  const int m = first < n ? min(kRegCand, (n - first + kThreads - 1) / kThreads) : 0;
+  wave_topk(
+      m, [&](int j, long long& key, int& song) { get(first + j * kThreads, key, song); }, k, wk + w * k, ws + w * k);
   __syncthreads();
-  stamp_at(sb, round0_slot);
-  long long* src_k = a_k;
-  int* src_s = a_s;
-  long long* dst_k = b_k;
-  int* dst_s = b_s;
-  while (true) {
-    auto from_src = [&](int i, long long& key, int& song) {
-      key = src_k[i];
-      song = src_s[i];
-    };
-    if (m <= C) {
-      select_round(m, k, from_src, slot, slot_hi, out_k, out_s);
-      __syncthreads();
-      return;
-    }
-    select_round(m, k, from_src, slot, slot_hi, dst_k, dst_s);
-    m = sel_out(m, k);
-    __syncthreads();
-    long long* tk = src_k; src_k = dst_k; dst_k = tk;
-    int* ts = src_s; src_s = dst_s; dst_s = ts;
-  }
+  if (w == 0) wave_merge_lists(kWaves, k, wk, ws, out_k, out_s);
+  __syncthreads();
+}
+
+constexpr int kMergeStageBytes = 32 * 1024;  // LDS staging of tile lists per merge pass
+__host__ __device__ inline int merge_lists_per_pass(int k) {
+  const int kk = k > 0 ? k : 1;
+  int l = kMergeStageBytes / (12 * kk);
+  return l > 256 ? 256 : (l < 2 ? 2 : l);
 }
 
 // sc1 (L2-coherent, agent-scope) stores/loads for the in-launch hand-off of
@@ -518,12 +496,8 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
-  int4* slot = reinterpret_cast<int4*>(smem_raw + L.slot);
-  int* slot_hi = reinterpret_cast<int*>(smem_raw + L.slot_hi);
-  long long* a_k = reinterpret_cast<long long*>(smem_raw + L.a_k);
-  int* a_s = reinterpret_cast<int*>(smem_raw + L.a_s);
-  long long* b_k = reinterpret_cast<long long*>(smem_raw + L.b_k);
-  int* b_s = reinterpret_cast<int*>(smem_raw + L.b_s);
+  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
+  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
   long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   int* flag = reinterpret_cast<int*>(smem_raw + L.flag);
@@ -663,14 +637,14 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   __syncthreads();
   MR_STAMP(3);
 
-  // Tile top-k -> fk/fs (LDS).
-  block_select(
+  // Tile top-k -> fk/fs (LDS): per-wave DPP rounds, then a 4-list tournament.
+  block_topk(
       bw, k,
       [&](int i, long long& key, int& song) {
         key = (long long)acc[i];
         song = blo + i;
       },
-      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, sb, 10);
+      wk, ws, fk, fs);
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
@@ -704,57 +678,32 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 #endif
   if (!*flag) return;
 
-  // Last tile of user u: top-k over all tiles' candidates (sc1 loads),
-  // staged into LDS region A with all loads in flight at once.
-  const int nc = p.n_tiles * k;
-  if (L.stage_cap >= nc) {
-    // Stage the candidates (one batch of sc1 loads) and the bound
-    // B = max over tiles of their k-th key: every tile holds k candidates
-    // >= its k-th key, so the user's k-th best is >= B and candidates below
-    // B are out. Survivors are compacted (order is irrelevant: ranks are exact).
-    const int scap = L.stage_cap;
+  // Last tile of user u: tournament over the tiles' sorted candidate lists,
+  // staged into LDS region A with sc1 loads (stage_lists lists per pass; the
+  // running top-k is list 0 of every later pass).
+  {
     long long* mk = reinterpret_cast<long long*>(smem_raw + L.acc);
-    int* ms = reinterpret_cast<int*>(smem_raw + L.acc + scap * 8);
-    long long* vk = reinterpret_cast<long long*>(smem_raw + L.acc + scap * 8 + align16(scap * 4));
-    int* vs = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(vk) + scap * 8);
-    unsigned long long* sbound = reinterpret_cast<unsigned long long*>(smem_raw + L.misc);
-    int* scount = reinterpret_cast<int*>(smem_raw + L.misc + 8);
-    if (tid == 0) { *sbound = 0ull; *scount = 0; }
-    __syncthreads();
-    for (int i = tid; i < nc; i += kThreads) {
-      const long long key = ld_sc1(&ck[i]);
-      mk[i] = key;
-      ms[i] = ld_sc1(&cs[i]);
-      if ((i % k) == k - 1 && key >= 0) atomicMax(sbound, (unsigned long long)key);
-    }
-    __syncthreads();
-    MR_STAMP(6);
-    const long long bound = (long long)*sbound;
-    for (int i = tid; i < nc; i += kThreads) {
-      if (mk[i] >= 0 && mk[i] >= bound) {
-        const int pos = atomicAdd(scount, 1);
-        vk[pos] = mk[i];
-        vs[pos] = ms[i];
+    int* ms = reinterpret_cast<int*>(smem_raw + L.acc + L.stage_lists * k * 8);
+    const int w = tid >> 6;
+    int done = 0, off = 0;
+    while (done < p.n_tiles) {
+      const int nl = min(p.n_tiles - done, L.stage_lists - off);
+      for (int i = tid; i < nl * k; i += kThreads) {
+        mk[off * k + i] = ld_sc1(&ck[(size_t)done * k + i]);
+        ms[off * k + i] = ld_sc1(&cs[(size_t)done * k + i]);
       }
+      for (int i = tid; i < off * k; i += kThreads) {
+        mk[i] = fk[i];
+        ms[i] = fs[i];
+      }
+      __syncthreads();
+      MR_STAMP(6);
+      if (w == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
+      __syncthreads();
+      MR_STAMP(8);
+      done += nl;
+      off = 1;
     }
-    __syncthreads();
-    MR_STAMP(7);
-    block_select(
-        *scount, k,
-        [&](int i, long long& key, int& song) {
-          key = vk[i];
-          song = vs[i];
-        },
-        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs, sb, 11);
-    MR_STAMP(8);
-  } else {
-    block_select(
-        nc, k,
-        [&](int i, long long& key, int& song) {
-          key = ld_sc1(&ck[i]);
-          song = ld_sc1(&cs[i]);
-        },
-        slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
   }
   for (int r = tid; r < k; r += kThreads) {
     const size_t o = (size_t)u * k + r;
@@ -780,40 +729,44 @@ struct MergeParams {
   double* out_scores;     // may be null
 };
 
-__host__ __device__ inline int merge_lds_bytes(int n, int k) {
-  const int C = 64 * sel_e(k);
-  const int cap = sel_out(n, k);
-  return align16(kWaves * C * 20) + 2 * align16(cap * 12) + align16(kMaxTopK * 12);
+__host__ __device__ inline int merge_lds_bytes(int k) {
+  return align16(merge_lists_per_pass(k) * k * 12) + align16(kMaxTopK * 12);
 }
 
 __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int k = p.k_out;
-  const int n = p.n_lists * p.k_in;
-  const int C = 64 * sel_e(k);
-  const int cap = sel_out(n, k);
-  int4* slot = reinterpret_cast<int4*>(smem_raw);
-  int* slot_hi = reinterpret_cast<int*>(smem_raw + kWaves * C * 16);
-  long long* a_k = reinterpret_cast<long long*>(smem_raw + align16(kWaves * C * 20));
-  int* a_s = reinterpret_cast<int*>(a_k + cap);
-  long long* b_k = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(a_k) + align16(cap * 12));
-  int* b_s = reinterpret_cast<int*>(b_k + cap);
-  long long* fk = reinterpret_cast<long long*>(reinterpret_cast<unsigned char*>(b_k) + align16(cap * 12));
+  const int per = merge_lists_per_pass(k);
+  long long* mk = reinterpret_cast<long long*>(smem_raw);
+  int* ms = reinterpret_cast<int*>(mk + per * k);
+  long long* fk = reinterpret_cast<long long*>(smem_raw + align16(per * k * 12));
   int* fs = reinterpret_cast<int*>(fk + kMaxTopK);
   const int bu = blockIdx.x;
+  const int tid = threadIdx.x;
   const long long* keys = p.keys + (size_t)bu * p.user_stride;
   const int* songs = p.songs + (size_t)bu * p.user_stride;
-  block_select(
-      n, k,
-      [&](int i, long long& key, int& song) {
-        const int l = i / p.k_in, r = i - l * p.k_in;
-        const size_t off = (size_t)l * p.list_stride + r;
-        key = keys[off];
-        song = songs[off];
-      },
-      slot, slot_hi, a_k, a_s, b_k, b_s, fk, fs);
-  const size_t o = (size_t)bu * p.k_out;
-  for (int r = threadIdx.x; r < p.k_out; r += kThreads) {
+  int done = 0, off = 0;
+  while (done < p.n_lists) {
+    const int nl = min(p.n_lists - done, per - off);
+    for (int i = tid; i < nl * k; i += kThreads) {
+      const int l = done + i / k, r = i - (i / k) * k;
+      const bool in = r < p.k_in;
+      const size_t src = (size_t)l * p.list_stride + r;
+      mk[off * k + i] = in ? keys[src] : kKeyNone;
+      ms[off * k + i] = in ? songs[src] : -1;
+    }
+    for (int i = tid; i < off * k; i += kThreads) {
+      mk[i] = fk[i];
+      ms[i] = fs[i];
+    }
+    __syncthreads();
+    if ((tid >> 6) == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
+    __syncthreads();
+    done += nl;
+    off = 1;
+  }
+  const size_t o = (size_t)bu * k;
+  for (int r = tid; r < k; r += kThreads) {
     p.out_keys[o + r] = fk[r];
     p.out_songs[o + r] = fs[r];
     if (p.out_scores) p.out_scores[o + r] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
@@ -919,9 +872,10 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
 }
 
 int auto_block_songs(int width, int n_te, bool fused, int k) {
-  // Aim for >= ~1024 workgroups, tiles of 256..8192 songs (16384 only
-  // without top-k: the selection buffers share the LDS with the tile).
-  const long long cap = (fused || k > 0) ? 8192 : kMaxBlockSongs;
+  // Aim for >= ~1024 workgroups, tiles of 256..16384 songs; with top-k a tile
+  // is at most kMaxTopkTile songs (4 candidates per lane in registers); the
+  // fused path keeps the neighbour array beside the tile (<= 8192).
+  const long long cap = k > 0 ? kMaxTopkTile : (fused ? 8192 : kMaxBlockSongs);
   long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
   long long bs = ((want + 255) / 256) * 256;
   bs = std::max<long long>(256, std::min<long long>(cap, bs));
@@ -1065,6 +1019,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
   const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, c->opt.topk);
   if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
+  if (c->opt.topk > 0 && bs > kMaxTopkTile)
+    return fail(MR_E_INVALID, "with topk > 0 block_songs must be <= %d (got %d)", kMaxTopkTile, bs);
   const int n_tiles = (width + bs - 1) / bs;
   const int k = c->opt.topk;
   // Per-song / per-user fixed-point tables, computed once on the host with
@@ -1331,7 +1287,7 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   MR_HIP(hipSetDevice(c->opt.device));
   MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
                  reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
-  const int lds = merge_lds_bytes(n_shards * k, k);
+  const int lds = merge_lds_bytes(k);
   if (lds > 160 * 1024) return fail(MR_E_INVALID, "merge of %d lists x %d needs too much LDS", n_shards, k);
   MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL(k_topk_merge, dim3(n_te), dim3(kThreads), lds, c->stream, mp);

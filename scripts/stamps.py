@@ -47,13 +47,10 @@ def phase(name, a, b, rows=None):
 phase("stage1", 0, 1)
 phase("stage2", 1, 2)
 phase("epilogue", 2, 3)
-phase("tile-topk round0", 3, 10)
-phase("tile-topk final", 10, 4)
+phase("tile-topk", 3, 4)
 phase("handoff", 4, 5)
 phase("merge stage", 5, 6, last)
-phase("merge compact", 6, 7, last)
-phase("merge select r0", 7, 11, last)
-phase("merge select fin", 11, 8, last)
+phase("merge tournament", 6, 8, last)
 phase("merge write", 8, 9, last)
 end = np.where(last, rt[:, 9], rt[:, 5])
 print("WG end offsets (us) min/med/max", *np.round(np.percentile(end - t0, [0, 50, 100]), 2))

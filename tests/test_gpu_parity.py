@@ -71,14 +71,18 @@ def test_golden_fixture(name, model):
 
 
 @pytest.mark.parametrize("stage1", ["fused", "separate"])
-@pytest.mark.parametrize("block", [256, 512, 768, 8192, 16384])
+@pytest.mark.parametrize("block", [256, 512, 768, 1024, 2048, 8192, 16384])
 @pytest.mark.parametrize("model", MODELS)
 def test_tile_sizes_bit_identical(block, model, stage1):
     ds, _ = synth_fixture("small")
-    if block > 8192:  # the top-k selection buffers no longer fit next to the tile
+    if block > 1024:  # top-k tiles hold <= 1024 songs; dense-only tiles may be larger
         with pytest.raises(_lib.EngineError):
             Engine(ds, block_songs=block, stage1=stage1)
-        with Engine(ds, block_songs=block, stage1="separate", topk=0, out_dtype="f64") as e:
+        if stage1 == "fused" and block > 8192:
+            with pytest.raises(_lib.EngineError):
+                Engine(ds, block_songs=block, stage1=stage1, topk=0)
+            return
+        with Engine(ds, block_songs=block, stage1=stage1, topk=0, out_dtype="f64") as e:
             got = e.score_dense(model)
         assert np.array_equal(got, native.fp_model(ds, model)[0], equal_nan=True)
         return
