@@ -176,117 +176,161 @@ __device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, 
 // Top-k selection, all in registers + DPP (no LDS round trips on the chain).
 // ---------------------------------------------------------------------------
 
-// One step of a wave argmax: take the better of my candidate and the one the
-// DPP pattern CTRL routes to me (invalid sources keep my own: idempotent).
+// 32-bit wave reductions on DPP: row_shr 1/2/4/8 leave each row's result in
+// its lane 15, row_bcast 15/31 carry the rows into lane 63, readlane
+// broadcasts it (as an SGPR value) to the whole wave. Sources outside a row
+// keep the lane's own value (idempotent ops only).
 template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ void argmax_step(long long& k, int& s) {
-  const int lo = (int)(unsigned)(k & 0xffffffffll), hi = (int)(k >> 32);
-  const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false);
-  const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false);
-  const int s2 = __builtin_amdgcn_update_dpp(s, s, CTRL, ROW_MASK, 0xf, false);
-  const long long k2 = (long long)(((unsigned long long)(unsigned)hi2 << 32) | (unsigned)lo2);
-  if (cand_before(k2, s2, k, s)) { k = k2; s = s2; }
+__device__ __forceinline__ int dpp(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ int wave_max_i32(int x) {
+  x = max(x, dpp<0x111, 0xf>(x));
+  x = max(x, dpp<0x112, 0xf>(x));
+  x = max(x, dpp<0x114, 0xf>(x));
+  x = max(x, dpp<0x118, 0xf>(x));
+  x = max(x, dpp<0x142, 0xa>(x));
+  x = max(x, dpp<0x143, 0xc>(x));
+  return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
+  x = max(x, (unsigned)dpp<0x111, 0xf>((int)x));
+  x = max(x, (unsigned)dpp<0x112, 0xf>((int)x));
+  x = max(x, (unsigned)dpp<0x114, 0xf>((int)x));
+  x = max(x, (unsigned)dpp<0x118, 0xf>((int)x));
+  x = max(x, (unsigned)dpp<0x142, 0xa>((int)x));
+  x = max(x, (unsigned)dpp<0x143, 0xc>((int)x));
+  return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ int wave_min_i32(int x) {
+  x = min(x, dpp<0x111, 0xf>(x));
+  x = min(x, dpp<0x112, 0xf>(x));
+  x = min(x, dpp<0x114, 0xf>(x));
+  x = min(x, dpp<0x118, 0xf>(x));
+  x = min(x, dpp<0x142, 0xa>(x));
+  x = min(x, dpp<0x143, 0xc>(x));
+  return __builtin_amdgcn_readlane(x, 63);
 }
 
-// Wave-wide best candidate, returned (wave-uniform) to every lane:
-// row_shr 1/2/4/8 leave each row's best in its lane 15, row_bcast 15/31
-// carry the rows into lane 63, readlane broadcasts it.
+// Wave-wide best candidate in the (key desc, song asc) order, returned to
+// every lane: max of the high key words, then max of the low words among
+// those, then min song among those — three branch-free 32-bit reductions.
+// "No candidate" is (-1, INT_MAX): its high word -1 is below every valid one.
 __device__ __forceinline__ void wave_argmax(long long& k, int& s) {
-  argmax_step<0x111, 0xf>(k, s);  // row_shr:1
-  argmax_step<0x112, 0xf>(k, s);  // row_shr:2
-  argmax_step<0x114, 0xf>(k, s);  // row_shr:4
-  argmax_step<0x118, 0xf>(k, s);  // row_shr:8
-  argmax_step<0x142, 0xa>(k, s);  // row_bcast:15 -> rows 1, 3
-  argmax_step<0x143, 0xc>(k, s);  // row_bcast:31 -> rows 2, 3
-  const int lo = __builtin_amdgcn_readlane((int)(unsigned)(k & 0xffffffffll), 63);
-  const int hi = __builtin_amdgcn_readlane((int)(k >> 32), 63);
-  s = __builtin_amdgcn_readlane(s, 63);
-  k = (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+  const int hi = (int)(k >> 32);
+  const unsigned lo = (unsigned)(k & 0xffffffffll);
+  const int H = wave_max_i32(hi);
+  const unsigned Lo = wave_max_u32(hi == H ? lo : 0u);
+  const int S = wave_min_i32((hi == H && lo == Lo) ? s : INT_MAX);
+  k = (long long)(((unsigned long long)(unsigned)H << 32) | Lo);
+  s = S;
 }
 
-constexpr int kRegCand = 4;  // candidates per lane kept in registers
+// Branch-free "take b if it comes first".
+__device__ __forceinline__ void take_if_before(long long& ka, int& sa, long long kb, int sb) {
+  const bool t = cand_before(kb, sb, ka, sa);
+  ka = t ? kb : ka;
+  sa = t ? sb : sa;
+}
 
-// A wave's top-k: round r takes the best candidate strictly after round
-// r-1's winner in the total order (candidates are distinct songs, so no
-// "taken" marks). Lane l supplies m <= kRegCand candidates via get(j, ...),
-// loaded once into registers; key < 0 = no candidate. Lane 0 writes the
-// sorted list to out_k/out_s[0..k); missing slots (-1, -1).
-template <typename Get>
-__device__ __forceinline__ void wave_topk(int m, Get get, int k, long long* out_k, int* out_s) {
-  const int lane = threadIdx.x & 63;
-  long long rk[kRegCand];
-  int rs[kRegCand];
+// Sort M register candidates of a lane descending (odd-even transposition).
+template <int M>
+__device__ __forceinline__ void lane_sort(long long (&rk)[M], int (&rs)[M]) {
 #pragma unroll
-  for (int j = 0; j < kRegCand; ++j) {
-    rk[j] = kKeyNone;
-    rs[j] = INT_MAX;
-    if (j < m) get(j, rk[j], rs[j]);
-    if (rk[j] < 0) { rk[j] = kKeyNone; rs[j] = INT_MAX; }
+  for (int round = 0; round < M; ++round) {
+#pragma unroll
+    for (int j = round & 1; j + 1 < M; j += 2) {
+      const bool sw = cand_before(rk[j + 1], rs[j + 1], rk[j], rs[j]);
+      const long long k0 = rk[j], k1 = rk[j + 1];
+      const int s0 = rs[j], s1 = rs[j + 1];
+      rk[j] = sw ? k1 : k0;
+      rk[j + 1] = sw ? k0 : k1;
+      rs[j] = sw ? s1 : s0;
+      rs[j + 1] = sw ? s0 : s1;
+    }
   }
-  long long pk = LLONG_MAX;
-  int ps = -1;
+}
+
+// One wave's top-k from M register candidates per lane (any order; key < 0
+// = none): sort each lane's M, then k rounds of "argmax of the lane heads,
+// the winning lane shifts its list". Lane 0 writes out_k/out_s[0..k),
+// missing slots (-1, -1).
+template <int M>
+__device__ __forceinline__ void wave_topk_regs(long long (&rk)[M], int (&rs)[M], int k, long long* out_k,
+                                               int* out_s) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < M; ++j)
+    if (rk[j] < 0) { rk[j] = kKeyNone; rs[j] = INT_MAX; }
+  lane_sort<M>(rk, rs);
   int r = 0;
   for (; r < k; ++r) {
-    long long bk = kKeyNone;
-    int bs = INT_MAX;
-#pragma unroll
-    for (int j = 0; j < kRegCand; ++j)
-      if (rk[j] >= 0 && cand_before(pk, ps, rk[j], rs[j]) && cand_before(rk[j], rs[j], bk, bs)) {
-        bk = rk[j];
-        bs = rs[j];
-      }
+    long long bk = rk[0];
+    int bs = rs[0];
     wave_argmax(bk, bs);
     if (bk < 0) break;  // wave-uniform
     if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
-    pk = bk;
-    ps = bs;
+    const bool win = rk[0] == bk && rs[0] == bs;  // songs are unique: one winner
+#pragma unroll
+    for (int j = 0; j + 1 < M; ++j) {
+      rk[j] = win ? rk[j + 1] : rk[j];
+      rs[j] = win ? rs[j + 1] : rs[j];
+    }
+    rk[M - 1] = win ? kKeyNone : rk[M - 1];
+    rs[M - 1] = win ? INT_MAX : rs[M - 1];
   }
   for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
 }
 
-// Tournament over L sorted lists (desc, (-1,-1)-padded) of length k in LDS,
-// run by ONE wave: lane l owns lists l, l+64, l+128, l+192 and their heads;
-// each round the wave argmax of the heads is the next winner and its owner
-// advances that list. Lane 0 writes the merged top-k to out_k/out_s.
+// Tournament over L <= 256 sorted lists (desc, (-1,-1)-padded) of length k
+// in LDS, run by ONE wave: lane l owns lists l, l+64, l+128, l+192, keeps
+// each head and the element after it in registers (the LDS read for the
+// next-but-one is issued when a list advances and is needed one win later).
 __device__ __forceinline__ void wave_merge_lists(int L, int k, const long long* lk, const int* ls,
                                                  long long* out_k, int* out_s) {
   const int lane = threadIdx.x & 63;
   int pos[4];
-  long long hk[4];
-  int hs[4];
+  long long hk[4], nk[4];
+  int hs[4], ns[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int l = lane + 64 * j;
     pos[j] = 0;
-    hk[j] = kKeyNone;
-    hs[j] = INT_MAX;
+    hk[j] = nk[j] = kKeyNone;
+    hs[j] = ns[j] = INT_MAX;
     if (l < L) {
       hk[j] = lk[(size_t)l * k];
       hs[j] = ls[(size_t)l * k];
-      if (hk[j] < 0) { hk[j] = kKeyNone; hs[j] = INT_MAX; }
+      if (k > 1) {
+        nk[j] = lk[(size_t)l * k + 1];
+        ns[j] = ls[(size_t)l * k + 1];
+      }
     }
+    if (hk[j] < 0) { hk[j] = kKeyNone; hs[j] = INT_MAX; }
+    if (nk[j] < 0) { nk[j] = kKeyNone; ns[j] = INT_MAX; }
   }
   int r = 0;
   for (; r < k; ++r) {
-    long long bk = kKeyNone;
-    int bs = INT_MAX;
+    long long bk = hk[0];
+    int bs = hs[0];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (cand_before(hk[j], hs[j], bk, bs)) { bk = hk[j]; bs = hs[j]; }
+    for (int j = 1; j < 4; ++j) take_if_before(bk, bs, hk[j], hs[j]);
     wave_argmax(bk, bs);
     if (bk < 0) break;  // wave-uniform
     if (lane == 0) { out_k[r] = bk; out_s[r] = bs; }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (hk[j] == bk && hs[j] == bs) {  // songs are unique: exactly one owner
-        const int l = lane + 64 * j;
+      if (hk[j] == bk && hs[j] == bs) {  // the owner advances this list
+        hk[j] = nk[j];
+        hs[j] = ns[j];
         ++pos[j];
-        hk[j] = kKeyNone;
-        hs[j] = INT_MAX;
-        if (pos[j] < k) {
-          hk[j] = lk[(size_t)l * k + pos[j]];
-          hs[j] = ls[(size_t)l * k + pos[j]];
-          if (hk[j] < 0) { hk[j] = kKeyNone; hs[j] = INT_MAX; }
+        nk[j] = kKeyNone;
+        ns[j] = INT_MAX;
+        if (pos[j] + 1 < k) {
+          const int l = lane + 64 * j;
+          nk[j] = lk[(size_t)l * k + pos[j] + 1];
+          ns[j] = ls[(size_t)l * k + pos[j] + 1];
+          if (nk[j] < 0) { nk[j] = kKeyNone; ns[j] = INT_MAX; }
         }
       }
     }
@@ -294,17 +338,37 @@ __device__ __forceinline__ void wave_merge_lists(int L, int k, const long long* 
   for (int i = r + lane; i < k; i += 64) { out_k[i] = kKeyNone; out_s[i] = -1; }
 }
 
-// Block top-k of n <= 4 * 256 candidates get(i) into out (LDS): every wave
-// selects from its elements i = w*64 + lane + 256 j, then wave 0 merges the
-// four sorted wave lists. All threads call it; it ends with a barrier.
+// Block top-k of n <= 1024 candidates get(i) into out (LDS). n <= 256: one
+// wave holds 4 per lane and selects alone; otherwise every wave selects from
+// its 256 (i = w*64 + lane + 256 j), then wave 0 merges the 4 sorted lists.
+// All threads call it; it ends with a barrier.
 template <typename Get>
 __device__ __forceinline__ void block_topk(int n, int k, Get get, long long* wk, int* ws, long long* out_k,
                                            int* out_s) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int first = w * 64 + lane;
-  const int m = first < n ? min(kRegCand, (n - first + kThreads - 1) / kThreads) : 0;
-  wave_topk(
-      m, [&](int j, long long& key, int& song) { get(first + j * kThreads, key, song); }, k, wk + w * k, ws + w * k);
+  long long rk[4];
+  int rs[4];
+  if (n <= 256) {
+    if (w == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rk[j] = kKeyNone;
+        rs[j] = INT_MAX;
+        if (lane + 64 * j < n) get(lane + 64 * j, rk[j], rs[j]);
+      }
+      wave_topk_regs<4>(rk, rs, k, out_k, out_s);
+    }
+    __syncthreads();
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = w * 64 + lane + kThreads * j;
+    rk[j] = kKeyNone;
+    rs[j] = INT_MAX;
+    if (i < n) get(i, rk[j], rs[j]);
+  }
+  wave_topk_regs<4>(rk, rs, k, wk + w * k, ws + w * k);
   __syncthreads();
   if (w == 0) wave_merge_lists(kWaves, k, wk, ws, out_k, out_s);
   __syncthreads();
