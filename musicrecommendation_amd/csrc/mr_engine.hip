@@ -180,35 +180,32 @@ __device__ __forceinline__ bool cand_before(long long ka, int sa, long long kb, 
 // its lane 15, row_bcast 15/31 carry the rows into lane 63, readlane
 // broadcasts it (as an SGPR value) to the whole wave. Sources outside a row
 // keep the lane's own value (idempotent ops only).
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ int dpp(int x) {
-  return __builtin_amdgcn_update_dpp(x, x, CTRL, ROW_MASK, 0xf, false);
-}
+// One DPP reduction step as a single VALU op: x = op(x[src lane], x). Lanes
+// whose source is outside the row/pattern are not written (bound_ctrl off),
+// i.e. keep x: right for idempotent ops. The s_nop covers the VALU-write ->
+// DPP-read hazard the compiler cannot see through inline asm.
+#define MR_DPP(op, x, mod) asm volatile("s_nop 1\n\t" op " %0, %0, %0 " mod : "+v"(x))
+#define MR_DPP_REDUCE(op, x)                                          \
+  do {                                                                \
+    MR_DPP(op, x, "row_shr:1 row_mask:0xf bank_mask:0xf");            \
+    MR_DPP(op, x, "row_shr:2 row_mask:0xf bank_mask:0xf");            \
+    MR_DPP(op, x, "row_shr:4 row_mask:0xf bank_mask:0xf");            \
+    MR_DPP(op, x, "row_shr:8 row_mask:0xf bank_mask:0xf");            \
+    MR_DPP(op, x, "row_bcast:15 row_mask:0xa bank_mask:0xf");         \
+    MR_DPP(op, x, "row_bcast:31 row_mask:0xc bank_mask:0xf");         \
+    asm volatile("s_nop 1" ::: "memory");                             \
+  } while (0)
+
 __device__ __forceinline__ int wave_max_i32(int x) {
-  x = max(x, dpp<0x111, 0xf>(x));
-  x = max(x, dpp<0x112, 0xf>(x));
-  x = max(x, dpp<0x114, 0xf>(x));
-  x = max(x, dpp<0x118, 0xf>(x));
-  x = max(x, dpp<0x142, 0xa>(x));
-  x = max(x, dpp<0x143, 0xc>(x));
+  MR_DPP_REDUCE("v_max_i32_dpp", x);
   return __builtin_amdgcn_readlane(x, 63);
 }
 __device__ __forceinline__ unsigned wave_max_u32(unsigned x) {
-  x = max(x, (unsigned)dpp<0x111, 0xf>((int)x));
-  x = max(x, (unsigned)dpp<0x112, 0xf>((int)x));
-  x = max(x, (unsigned)dpp<0x114, 0xf>((int)x));
-  x = max(x, (unsigned)dpp<0x118, 0xf>((int)x));
-  x = max(x, (unsigned)dpp<0x142, 0xa>((int)x));
-  x = max(x, (unsigned)dpp<0x143, 0xc>((int)x));
+  MR_DPP_REDUCE("v_max_u32_dpp", x);
   return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
 }
 __device__ __forceinline__ int wave_min_i32(int x) {
-  x = min(x, dpp<0x111, 0xf>(x));
-  x = min(x, dpp<0x112, 0xf>(x));
-  x = min(x, dpp<0x114, 0xf>(x));
-  x = min(x, dpp<0x118, 0xf>(x));
-  x = min(x, dpp<0x142, 0xa>(x));
-  x = min(x, dpp<0x143, 0xc>(x));
+  MR_DPP_REDUCE("v_min_i32_dpp", x);
   return __builtin_amdgcn_readlane(x, 63);
 }
 
@@ -441,13 +438,13 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
     s_pre[tid] = pre;
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
-    // 8 flattened entries per thread in flight: the listener loads of one
+    // 16 flattened entries per thread in flight: the listener loads of one
     // batch are issued together, then their LDS atomics.
-    for (int i0 = tid; i0 < total; i0 += 8 * kThreads) {
-      int v[8];
-      unsigned long long wv[8];
+    for (int i0 = tid; i0 < total; i0 += 16 * kThreads) {
+      int v[16];
+      unsigned long long wv[16];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
+      for (int r = 0; r < 16; ++r) {
         const int i = i0 + r * kThreads;
         v[r] = -1;
         wv[r] = 0ull;
@@ -462,7 +459,7 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
         }
       }
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
+      for (int r = 0; r < 16; ++r)
         if (v[r] >= 0) atomicAdd(&Y[v[r]], wv[r]);
     }
     __syncthreads();
@@ -752,9 +749,28 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     int done = 0, off = 0;
     while (done < p.n_tiles) {
       const int nl = min(p.n_tiles - done, L.stage_lists - off);
-      for (int i = tid; i < nl * k; i += kThreads) {
-        mk[off * k + i] = ld_sc1(&ck[(size_t)done * k + i]);
-        ms[off * k + i] = ld_sc1(&cs[(size_t)done * k + i]);
+      // 4 candidates per thread in flight per batch (loads first, then LDS)
+      for (int i0 = tid; i0 < nl * k; i0 += 4 * kThreads) {
+        long long lk4[4];
+        int ls4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + r * kThreads;
+          lk4[r] = kKeyNone;
+          ls4[r] = -1;
+          if (i < nl * k) {
+            lk4[r] = ld_sc1(&ck[(size_t)done * k + i]);
+            ls4[r] = ld_sc1(&cs[(size_t)done * k + i]);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + r * kThreads;
+          if (i < nl * k) {
+            mk[off * k + i] = lk4[r];
+            ms[off * k + i] = ls4[r];
+          }
+        }
       }
       for (int i = tid; i < off * k; i += kThreads) {
         mk[i] = fk[i];
