@@ -210,17 +210,30 @@ __device__ __forceinline__ int wave_min_i32(int x) {
 }
 
 // Wave-wide best candidate in the (key desc, song asc) order, returned to
-// every lane: max of the high key words, then max of the low words among
-// those, then min song among those — three branch-free 32-bit reductions.
+// every lane: max of the high key words; if one lane holds it (the common
+// case) its low word and song are read with readlane, else max of the low
+// words among the tied lanes, then (if still tied) min song among those.
 // "No candidate" is (-1, INT_MAX): its high word -1 is below every valid one.
 __device__ __forceinline__ void wave_argmax(long long& k, int& s) {
   const int hi = (int)(k >> 32);
   const unsigned lo = (unsigned)(k & 0xffffffffll);
   const int H = wave_max_i32(hi);
-  const unsigned Lo = wave_max_u32(hi == H ? lo : 0u);
-  const int S = wave_min_i32((hi == H && lo == Lo) ? s : INT_MAX);
+  unsigned long long m = __ballot(hi == H);
+  unsigned Lo;
+  if (__popcll(m) == 1) {
+    const int l = __ffsll((long long)m) - 1;
+    Lo = (unsigned)__builtin_amdgcn_readlane((int)lo, l);
+    s = __builtin_amdgcn_readlane(s, l);
+  } else {
+    Lo = wave_max_u32(hi == H ? lo : 0u);
+    m = __ballot(hi == H && lo == Lo);
+    if (__popcll(m) == 1) {
+      s = __builtin_amdgcn_readlane(s, __ffsll((long long)m) - 1);
+    } else {
+      s = wave_min_i32((hi == H && lo == Lo) ? s : INT_MAX);
+    }
+  }
   k = (long long)(((unsigned long long)(unsigned)H << 32) | Lo);
-  s = S;
 }
 
 // Branch-free "take b if it comes first".
