@@ -104,7 +104,8 @@ typedef struct mr_options {
   int32_t out_dtype;   /* MR_OUT_F32 (default) or MR_OUT_F64 for the dense model */
   int32_t topk;        /* k of the per-test-user recommendation list (0 = off, <= 64; default 10) */
   int32_t dense;       /* 1 (default) = write the dense model; 0 = top-k only */
-  int32_t time_kernels;/* 1 = record HIP events around each kernel in mr_run (see mr_kernel_times) */
+  int32_t time_kernels;/* 1 = per-launch HIP events around each kernel in mr_run (diagnostic; they
+                          perturb back-to-back launches — see mr_kernel_times / mr_timing_begin) */
   int32_t stage1;      /* launch shape: 0 = auto, 1 = fused (one kernel; stage 1 recomputed per
                           song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel */
   int32_t reserved[6];
@@ -178,6 +179,13 @@ int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
  * fused stage 1 and the in-launch top-k merge —, 2 = reserved) the number of
  * timed launches and their summed device milliseconds; reset=1 clears. */
 int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
+
+/* Timing window: mr_timing_begin records an event on the context stream,
+ * mr_timing_end records a second one, waits for it and returns the device
+ * time between them and the number of scoring-kernel launches issued in
+ * between (no per-launch events: the window does not perturb the launches). */
+int mr_timing_begin(mr_ctx* ctx);
+int mr_timing_end(mr_ctx* ctx, int64_t* launches, double* total_ms);
 
 /* Diagnostic builds only (libmr_engine_stamps.so, -DMR_STAMPS): copy the
  * per-workgroup phase timestamps of the last scoring launch ([grid][8]

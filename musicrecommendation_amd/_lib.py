@@ -99,6 +99,8 @@ SIGNATURES = {
     "mr_topk_merge_device": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),
     "mr_debug_stamps": (c_int, [c_void_p, c_void_p, c_int64]),
+    "mr_timing_begin": (c_int, [c_void_p]),
+    "mr_timing_end": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double)]),
     "mr_stream": (c_void_p, [c_void_p]),
     "mr_last_error": (c_char_p, []),
     "mr_corpus_from_tsv": (c_int, [c_char_p, c_char_p, c_char_p, POINTER(c_void_p)]),

@@ -931,6 +931,11 @@ struct mr_ctx {
   bool ring_has_stage1[kRing] = {};
   long long launches[3] = {0, 0, 0};
   double ms[3] = {0, 0, 0};
+  // Timing window (mr_timing_begin/end): two events on the stream around any
+  // number of mr_run calls, no per-launch events.
+  hipEvent_t win[2] = {nullptr, nullptr};
+  bool win_open = false;
+  long long win_launches = 0;
 
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
@@ -1032,6 +1037,14 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
     delete c;
     return fail(MR_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
+  for (auto& ev : c->win) {
+    e = hipEventCreate(&ev);
+    if (e != hipSuccess) {
+      ev = nullptr;
+      mr_destroy(c);
+      return fail(MR_E_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+    }
+  }
   if (o.time_kernels) {
     c->ring.resize((size_t)mr_ctx::kRing * 3);
     for (auto& ev : c->ring) {
@@ -1053,6 +1066,7 @@ int mr_destroy(mr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->release_data();
   for (auto& ev : c->ring) if (ev) (void)hipEventDestroy(ev);
+  for (auto& ev : c->win) if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return MR_OK;
@@ -1284,6 +1298,7 @@ int run_model(mr_ctx* c, int model) {
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
+      if (c->win_open) c->win_launches++;
     }
     if (timed) MR_HIP(hipEventRecord(ev[2], st));
   }
@@ -1397,6 +1412,29 @@ int mr_debug_stamps(mr_ctx* c, int64_t* out, int64_t n) {
   MR_HIP(hipMemcpyAsync(out, c->stamps.p, m * 8, hipMemcpyDeviceToHost, c->stream));
   MR_HIP(hipStreamSynchronize(c->stream));
   return (int)MR_OK;
+}
+
+int mr_timing_begin(mr_ctx* c) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipEventRecord(c->win[0], c->stream));
+  c->win_open = true;
+  c->win_launches = 0;
+  return MR_OK;
+}
+
+int mr_timing_end(mr_ctx* c, int64_t* launches, double* total_ms) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->win_open) return fail(MR_E_STATE, "mr_timing_end without mr_timing_begin");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipEventRecord(c->win[1], c->stream));
+  MR_HIP(hipEventSynchronize(c->win[1]));
+  float t = 0.f;
+  MR_HIP(hipEventElapsedTime(&t, c->win[0], c->win[1]));
+  c->win_open = false;
+  if (launches) *launches = c->win_launches;
+  if (total_ms) *total_ms = t;
+  return MR_OK;
 }
 
 int mr_kernel_times(mr_ctx* c, int32_t which, int64_t* launches, double* total_ms, int32_t reset) {

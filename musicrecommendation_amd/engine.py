@@ -131,6 +131,17 @@ class Engine:
                                                 None, out_songs_ptr, out_keys_ptr, out_scores_ptr or None),
                    "mr_topk_merge_device")
 
+    def timing_begin(self) -> None:
+        """Open a timing window (one event on the engine stream)."""
+        _lib.check(self._L.mr_timing_begin(self._h), "mr_timing_begin")
+
+    def timing_end(self) -> Tuple[int, float]:
+        """Close the window: (scoring-kernel launches, device ms) since timing_begin."""
+        n = ctypes.c_int64()
+        ms = ctypes.c_double()
+        _lib.check(self._L.mr_timing_end(self._h, ctypes.byref(n), ctypes.byref(ms)), "mr_timing_end")
+        return n.value, ms.value
+
     def kernel_times(self, kernel: Union[str, int], reset: bool = False) -> Tuple[int, float]:
         n = ctypes.c_int64()
         ms = ctypes.c_double()
