@@ -207,7 +207,13 @@ def main() -> None:
         avg_us = win_ms / max(n_launch, 1) * 1e3
         achieved = ab_dom / (avg_us * 1e-6) / 1e9
         step_bytes = sum(ab_stage.values())
-        traffic = args.traffic_bytes
+        traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
+        pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+        if traffic is None and os.path.exists(pmc_file) and world == 1 and args.inflight == 1:
+            with open(pmc_file) as f:
+                pmc = json.load(f)
+            traffic = pmc.get("traffic_bytes_per_launch")
+            traffic_src = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command)"
         # quality companions on the last step's outputs (host-side, untimed)
         from musicrecommendation_amd import evaluation
 
@@ -250,6 +256,7 @@ def main() -> None:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": ab_dom,
                 "avg_launch_us": avg_us,
                 "timing": f"HIP events on the engine stream around the {args.steps} timed steps "
