@@ -249,8 +249,9 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_score (fused: stages 1+2+3, one launch per step)" if eng.fused
-                else "k_neighbours + k_score (per step)",
+                "kernel": {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
+                           "separate": "k_neighbours + k_score (per step)",
+                           "pull": "k_stage1_columns + k_pull + k_topk_merge (per step)"}[eng.shape],
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -262,7 +263,7 @@ def main() -> None:
                 "timing": f"HIP events on the engine stream around the {args.steps} timed steps "
                           f"({n_launch} scoring launches)",
             },
-            "launch": {"fused": eng.fused, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles},
+            "launch": {"shape": eng.shape, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles},
             "step_algorithmic_bytes": step_bytes,
             "step_GBps": step_bytes / (elapsed_max / args.steps) / 1e9,
             "mAP@10": map10,

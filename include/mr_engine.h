@@ -100,14 +100,19 @@ typedef struct mr_options {
   int32_t frac_bits;   /* fixed-point fraction bits F of the int64 accumulators (default 32, 8..40) */
   int32_t song_lo;     /* first song id of this context's shard (default 0) */
   int32_t song_hi;     /* one past the last song id; <= 0 means n_songs (default 0) */
-  int32_t block_songs; /* songs per LDS accumulator tile; 0 = auto (multiple of 256, <= 16384) */
+  int32_t block_songs; /* songs per LDS accumulator tile (pull shape: songs per range); 0 = auto
+                          (multiple of 256, <= 16384) */
   int32_t out_dtype;   /* MR_OUT_F32 (default) or MR_OUT_F64 for the dense model */
   int32_t topk;        /* k of the per-test-user recommendation list (0 = off, <= 64; default 10) */
   int32_t dense;       /* 1 (default) = write the dense model; 0 = top-k only */
   int32_t time_kernels;/* 1 = per-launch HIP events around each kernel in mr_run (diagnostic; they
                           perturb back-to-back launches — see mr_kernel_times / mr_timing_begin) */
   int32_t stage1;      /* launch shape: 0 = auto, 1 = fused (one kernel; stage 1 recomputed per
-                          song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel */
+                          song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel
+                          (compact neighbour lists), 3 = pull (stage 1 writes a dense
+                          Yt[train user][test user] slab, the scoring kernel gathers its rows per
+                          song; topk <= 16). Auto: pull from 256 test users, else fused when
+                          n_train_users <= 4096, else separate. */
   int32_t reserved[6];
 } mr_options;
 
@@ -127,9 +132,9 @@ int mr_load(mr_ctx* ctx, const mr_dataset* d);
  * test users. The dense model of this context is n_te x (song_hi - song_lo). */
 int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
 
-/* Launch shape chosen by mr_load: fused (1) or separate stage 1 (0), songs
- * per LDS tile and tiles per test user. */
-int mr_launch_info(const mr_ctx* ctx, int32_t* fused, int32_t* block_songs, int32_t* n_tiles);
+/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull; songs
+ * per LDS tile (pull: per song range) and tiles (ranges) per test user. */
+int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int32_t* n_tiles);
 
 /*
  * Score every (test user, song) pair of the shard for `model`, leaving the
@@ -175,8 +180,9 @@ int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
                          int32_t* songs_out, int64_t* keys_out, double* scores_out);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
- * (0 = separate stage-1 neighbour kernel, 1 = the scoring kernel — stage 2,
- * fused stage 1 and the in-launch top-k merge —, 2 = reserved) the number of
+ * (0 = separate stage-1 kernel — neighbour lists or pull columns —, 1 = the
+ * scoring kernels — stage 2, fused stage 1, the in-launch top-k merge, the pull
+ * kernel and its top-k merge —, 2 = reserved) the number of
  * timed launches and their summed device milliseconds; reset=1 clears. */
 int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
 
@@ -191,6 +197,11 @@ int mr_timing_end(mr_ctx* ctx, int64_t* launches, double* total_ms);
  * per-workgroup phase timestamps of the last scoring launch ([grid][8]
  * s_memrealtime values); MR_E_STATE in the production build. */
 int mr_debug_stamps(mr_ctx* ctx, int64_t* out, int64_t n);
+
+/* Diagnostic builds only (libmr_engine_checks.so, -DMR_CHECKS): bits of the
+ * array classes whose index went out of range in the pull-shape kernels since
+ * mr_load (0 = none); MR_E_STATE in the production build. */
+int mr_debug_checks(mr_ctx* ctx, uint32_t* bits);
 
 /* HIP stream of the context (as void* = hipStream_t). */
 void* mr_stream(const mr_ctx* ctx);

@@ -15,8 +15,10 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MR_ENGINE_LIB=stamps selects the diagnostic build (phase timestamps).
-LIB_PATH = os.path.join(_HERE, "libmr_engine_stamps.so" if os.environ.get("MR_ENGINE_LIB") == "stamps"
+# MR_ENGINE_LIB=stamps|checks selects a diagnostic build (phase timestamps /
+# bounds-checked pull kernels).
+_VARIANT = os.environ.get("MR_ENGINE_LIB", "")
+LIB_PATH = os.path.join(_HERE, f"libmr_engine_{_VARIANT}.so" if _VARIANT in ("stamps", "checks")
                         else "libmr_engine.so")
 
 MR_OK = 0
@@ -99,6 +101,7 @@ SIGNATURES = {
     "mr_topk_merge_device": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),
     "mr_debug_stamps": (c_int, [c_void_p, c_void_p, c_int64]),
+    "mr_debug_checks": (c_int, [c_void_p, c_void_p]),
     "mr_timing_begin": (c_int, [c_void_p]),
     "mr_timing_end": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double)]),
     "mr_stream": (c_void_p, [c_void_p]),

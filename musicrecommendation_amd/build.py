@@ -40,6 +40,7 @@ def _stale() -> bool:
 
 
 OUT_STAMPS = os.path.join(HERE, "libmr_engine_stamps.so")
+OUT_CHECKS = os.path.join(HERE, "libmr_engine_checks.so")
 
 
 def _compile(out: str, extra, verbose: bool) -> None:
@@ -52,11 +53,13 @@ def _compile(out: str, extra, verbose: bool) -> None:
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = True) -> str:
-    """Production library; plus the phase-timestamp diagnostic variant."""
+    """Production library; plus the diagnostic variants (phase timestamps,
+    bounds-checked pull kernels)."""
     if force or _stale():
         _compile(OUT, [], verbose)
         if stamps:
             _compile(OUT_STAMPS, ["-DMR_STAMPS"], verbose)
+            _compile(OUT_CHECKS, ["-DMR_CHECKS"], verbose)
     return OUT
 
 

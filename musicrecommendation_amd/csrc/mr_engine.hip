@@ -426,14 +426,14 @@ struct NbrParams {
 };
 
 // Accumulate Y[v] += w(s2) over v ∈ L_tr(s2), s2 ∈ T(u): a flattened walk over
-// the listener lists of T(u), 256 songs of T(u) at a time. If `heard` is
-// non-null, also mark T(u) ∩ [blo, bhi) in the tile's heard bitmap.
-template <int MODEL>
-__device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, long long t0, long long t1,
-                                                      const int* te_songs, const long long* trs_off,
-                                                      const int* trs_users, const long long* q_song,
-                                                      long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
-                                                      unsigned* heard, int blo, int bhi) {
+// the listener lists of T(u), 256 songs of T(u) at a time; add(v, w) performs
+// the (integer, order-independent) accumulation. mark(s2) is called once per
+// song of T(u) (heard-song bookkeeping).
+template <int MODEL, typename Add, typename Mark>
+__device__ __forceinline__ void walk_neighbours(long long t0, long long t1, const int* te_songs,
+                                                const long long* trs_off, const int* trs_users,
+                                                const long long* q_song, long long* s_lo, long long* s_w,
+                                                int* s_pre, int* s_scan, Add add, Mark mark) {
   const int tid = threadIdx.x;
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
@@ -444,7 +444,7 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
       len = (int)(trs_off[s2 + 1] - lo);
       s_lo[tid] = lo;
       s_w[tid] = (MODEL == MR_IBM) ? q_song[s2] : 1ll;
-      if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
+      mark(s2);
     }
     int total;
     const int pre = block_excl_scan(len, &total, s_scan);
@@ -452,7 +452,7 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
     // 16 flattened entries per thread in flight: the listener loads of one
-    // batch are issued together, then their LDS atomics.
+    // batch are issued together, then their accumulations.
     for (int i0 = tid; i0 < total; i0 += 16 * kThreads) {
       int v[16];
       unsigned long long wv[16];
@@ -473,10 +473,24 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (v[r] >= 0) atomicAdd(&Y[v[r]], wv[r]);
+        if (v[r] >= 0) add(v[r], wv[r]);
     }
     __syncthreads();
   }
+}
+
+template <int MODEL>
+__device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, long long t0, long long t1,
+                                                      const int* te_songs, const long long* trs_off,
+                                                      const int* trs_users, const long long* q_song,
+                                                      long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
+                                                      unsigned* heard, int blo, int bhi) {
+  walk_neighbours<MODEL>(
+      t0, t1, te_songs, trs_off, trs_users, q_song, s_lo, s_w, s_pre, s_scan,
+      [&](int v, unsigned long long w) { atomicAdd(&Y[v], w); },
+      [&](int s2) {
+        if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
+      });
 }
 
 // Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
@@ -587,8 +601,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const double two_f = ldexp(1.0, p.frac_bits);
 #ifdef MR_STAMPS
   long long* sb = p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr;
-#else
-  long long* sb = nullptr;
 #endif
   MR_STAMP(0);
 
@@ -809,6 +821,205 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// pull shape (dense neighbourhoods, e.g. 10k x 1k): stage 1 scatters the
+// neighbour weights of a batch of test users into Yt[v][user] (int64 global
+// atomics: exact and order-independent); a pull kernel then gives each wave
+// 64 users (lanes) and walks songs: acc[u] = Σ_{v ∈ L_tr(s)} Yt[v][u] is a
+// 512-byte coalesced row gather per listener, summed in registers (no
+// atomics, no tiles of accumulators). Scores go through a per-wave LDS tile
+// for row-contiguous stores; each lane keeps a running top-k of its user.
+// ---------------------------------------------------------------------------
+// Wave-private LDS hand-off: wait for this wave's LDS ops, keep the compiler
+// from reordering across it (a single wave needs no s_barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Bounds-checked diagnostic build (-DMR_CHECKS, libmr_engine_checks.so): an
+// out-of-range index is recorded in *dbg (bit = code) and replaced by 0.
+#ifdef MR_CHECKS
+#define MR_IDX(i, n, code) \
+  (((unsigned long long)(i) < (unsigned long long)(n)) ? (i) : (atomicOr(p.dbg, (code)), (decltype(i))0))
+#else
+#define MR_IDX(i, n, code) (i)
+#endif
+
+constexpr int kPullLanes = 64;   // users per wave
+constexpr int kPullChunk = 32;   // songs per staged output tile
+constexpr int kPullMaxK = 16;    // running top-k slots per lane (registers)
+constexpr int kPullMinUsers = 256;  // auto shape: pull from this many test users
+
+struct ColParams {
+  int n_tr, user0, te_stride, frac_bits;
+  const long long* te_off;
+  const int* te_songs;
+  const long long* trs_off;
+  const int* trs_users;
+  const long long* q_song;
+  const double* sqrt_tr;
+  const double* sqrt_te;
+  unsigned long long* Yt;    // [n_tr][te_stride]: column bu = batch user bu
+  unsigned* dbg;             // MR_CHECKS builds
+  long long n_yt;
+};
+
+// Stage 1 of the pull shape: one workgroup per test user accumulates Y[v] in
+// LDS (as k_neighbours) and stores the whole column Yt[.][bu], zeros
+// included, so Yt needs no clearing between runs. UBM weights are final
+// fixed-point cosines here (MR:142-148).
+template <int MODEL>
+__global__ __launch_bounds__(kThreads) void k_stage1_columns(ColParams p) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw);         // [n_tr]
+  long long* s_lo = reinterpret_cast<long long*>(smem_raw + align16(p.n_tr * 8));  // [256]
+  long long* s_w = s_lo + kThreads;                                                // [256]
+  int* s_pre = reinterpret_cast<int*>(s_w + kThreads);                             // [257]
+  int* s_scan = s_pre + kThreads + 4;                                              // [kWaves]
+  const int bu = blockIdx.x;
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+  __syncthreads();
+  accumulate_neighbours<MODEL>(Y, p.te_off[u], p.te_off[u + 1], p.te_songs, p.trs_off, p.trs_users, p.q_song,
+                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0);
+  const double two_f = ldexp(1.0, p.frac_bits);
+  const double rs_u = p.sqrt_te[u];
+  unsigned long long* col = p.Yt + bu;
+  for (int v = tid; v < p.n_tr; v += kThreads) {
+    const unsigned long long y = Y[v];
+    col[MR_IDX((size_t)v * p.te_stride + bu, (size_t)p.n_yt, 1u) - bu] =
+        y ? (unsigned long long)neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f) : 0ull;
+  }
+}
+
+struct PullParams {
+  int user0, n_users, te_stride;
+  int song_lo, song_hi, width, range, n_ranges;
+  int frac_bits, topk, dense;
+  const unsigned long long* Yt;
+  const long long* trs_off;
+  const int* trs_users;
+  const double* sqrt_c;
+  const long long* te_off;       // heard songs: the sorted T(u), walked per lane
+  const int* te_songs;
+  void* dense_out;               // [n_te][width]
+  long long* cand_key;           // [te_stride][n_ranges][k] (batch-local users)
+  int* cand_song;
+  unsigned* dbg;                 // MR_CHECKS builds: sizes of the arrays above
+  long long n_yt, n_trs, n_te_songs, n_te_off, n_songs1, n_dense, n_cand;
+};
+
+template <int MODEL, typename OutT>
+__global__ __launch_bounds__(kThreads) void k_pull(PullParams p) {
+  __shared__ OutT tile[kWaves][kPullLanes][kPullChunk + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int range = blockIdx.x;
+  const int bu0 = (blockIdx.y * kWaves + w) * kPullLanes;  // this wave's first batch user
+  if (bu0 >= p.n_users) return;                              // whole wave idle (wave-uniform)
+  const int bu = bu0 + lane;
+  const bool uok = bu < p.n_users;
+  const int s_begin = p.song_lo + range * p.range;
+  const int s_end = min(p.song_hi, s_begin + p.range);
+  const double inv_f = ldexp(1.0, -p.frac_bits);
+  const unsigned long long* yrow = p.Yt + bu0 + lane;       // + v * te_stride
+  // next heard song of this lane's user at or after s_begin (songs ascend)
+  long long hp = 0, hend = 0;
+  if (uok) {
+    long long a = p.te_off[MR_IDX(p.user0 + bu, p.n_te_off, 2u)], b = p.te_off[MR_IDX(p.user0 + bu + 1, p.n_te_off, 2u)];
+    hend = b;
+    while (a < b) {
+      const long long m = (a + b) >> 1;
+      if (p.te_songs[MR_IDX(m, p.n_te_songs, 4u)] < s_begin) a = m + 1; else b = m;
+    }
+    hp = a;
+  }
+  int next_heard = hp < hend ? p.te_songs[MR_IDX(hp, p.n_te_songs, 4u)] : INT_MAX;
+  OutT (*tw)[kPullChunk + 1] = tile[w];
+  const int k = p.topk;
+  long long tk[kPullMaxK];
+  int ts[kPullMaxK];
+#pragma unroll
+  for (int j = 0; j < kPullMaxK; ++j) { tk[j] = kKeyNone; ts[j] = INT_MAX; }
+  long long thr = kKeyNone;  // current k-th key of this lane's list
+
+  for (int c0 = s_begin; c0 < s_end; c0 += kPullChunk) {
+    const int cn = min(kPullChunk, s_end - c0);
+    for (int j = 0; j < cn; ++j) {
+      const int s = c0 + j;
+      const long long x0 = p.trs_off[MR_IDX(s, p.n_songs1, 8u)], x1 = p.trs_off[MR_IDX(s + 1, p.n_songs1, 8u)];
+      unsigned long long acc = 0ull;
+      long long x = x0;
+      for (; x + 4 <= x1; x += 4) {  // 4 row gathers in flight
+        const int v0 = p.trs_users[MR_IDX(x, p.n_trs, 16u)], v1 = p.trs_users[MR_IDX(x + 1, p.n_trs, 16u)];
+        const int v2 = p.trs_users[MR_IDX(x + 2, p.n_trs, 16u)], v3 = p.trs_users[MR_IDX(x + 3, p.n_trs, 16u)];
+        const size_t yo = bu0 + lane;
+        const unsigned long long a0 = yrow[MR_IDX((size_t)v0 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
+        const unsigned long long a1 = yrow[MR_IDX((size_t)v1 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
+        const unsigned long long a2 = yrow[MR_IDX((size_t)v2 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
+        const unsigned long long a3 = yrow[MR_IDX((size_t)v3 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
+        acc += (a0 + a1) + (a2 + a3);
+      }
+      for (; x < x1; ++x) {
+        const size_t yo = bu0 + lane;
+        const int v = p.trs_users[MR_IDX(x, p.n_trs, 16u)];
+        acc += yrow[MR_IDX((size_t)v * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
+      }
+      double score = (double)(long long)acc * inv_f;
+      if (MODEL == MR_IBM) score = score / p.sqrt_c[s];
+      const bool h = s == next_heard;
+      if (h) {
+        ++hp;
+        next_heard = hp < hend ? p.te_songs[MR_IDX(hp, p.n_te_songs, 4u)] : INT_MAX;
+      }
+      tw[lane][j] = h ? (OutT)NAN : (OutT)score;
+      // running top-k: songs arrive in increasing order, so an equal key never
+      // displaces an earlier (lower-id) song
+      const long long key = h ? kKeyNone : __double_as_longlong(score);
+      if (k > 0 && key > thr) {
+        long long ck = key;
+        int cs = s;
+#pragma unroll
+        for (int t = 0; t < kPullMaxK; ++t) {
+          const bool b = t < k && cand_before(ck, cs, tk[t], ts[t]);
+          const long long ok = tk[t];
+          const int os = ts[t];
+          tk[t] = b ? ck : tk[t];
+          ts[t] = b ? cs : ts[t];
+          ck = b ? ok : ck;
+          cs = b ? os : cs;
+        }
+        long long nt = kKeyNone;
+#pragma unroll
+        for (int t = 0; t < kPullMaxK; ++t) nt = (t == k - 1) ? tk[t] : nt;
+        thr = nt;
+      }
+    }
+    if (p.dense) {  // flush the wave's [64 users][cn songs] tile, two rows per store
+      wave_lds_sync();
+      OutT* out = reinterpret_cast<OutT*>(p.dense_out);
+      const int r_half = lane >> 5, col = lane & 31;
+      for (int r0 = 0; r0 < kPullLanes; r0 += 2) {
+        const int r = r0 + r_half;
+        if (bu0 + r < p.n_users && col < cn)
+          out[MR_IDX((size_t)(p.user0 + bu0 + r) * p.width + (c0 - p.song_lo) + col, (size_t)p.n_dense, 64u)] =
+              tw[r][col];
+      }
+      wave_lds_sync();
+    }
+  }
+  if (k > 0 && uok) {
+    const size_t co = MR_IDX(((size_t)bu * p.n_ranges + range) * k + (k - 1), (size_t)p.n_cand, 128u) - (k - 1);
+    long long* ck = p.cand_key + co;
+    int* cs = p.cand_song + co;
+#pragma unroll
+    for (int t = 0; t < kPullMaxK; ++t)
+      if (t < k) { ck[t] = tk[t]; cs[t] = tk[t] >= 0 ? ts[t] : -1; }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Top-k merge over lists (exchange step after a song-shard all-gather).
 // Element (u, l, r) of the input sits at u*user_stride + l*list_stride + r.
 // ---------------------------------------------------------------------------
@@ -820,6 +1031,8 @@ struct MergeParams {
   long long* out_keys;    // [n_users][k_out]
   int* out_songs;
   double* out_scores;     // may be null
+  unsigned* dbg;          // MR_CHECKS builds (0 sizes = unchecked)
+  long long n_in, n_out;
 };
 
 __host__ __device__ inline int merge_lds_bytes(int k) {
@@ -844,7 +1057,10 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
     for (int i = tid; i < nl * k; i += kThreads) {
       const int l = done + i / k, r = i - (i / k) * k;
       const bool in = r < p.k_in;
-      const size_t src = (size_t)l * p.list_stride + r;
+      size_t src = (size_t)l * p.list_stride + r;
+#ifdef MR_CHECKS
+      if (p.n_in && in) src = MR_IDX(src + (size_t)bu * p.user_stride, (size_t)p.n_in, 256u) - (size_t)bu * p.user_stride;
+#endif
       mk[off * k + i] = in ? keys[src] : kKeyNone;
       ms[off * k + i] = in ? songs[src] : -1;
     }
@@ -858,7 +1074,10 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
     done += nl;
     off = 1;
   }
-  const size_t o = (size_t)bu * k;
+  size_t o = (size_t)bu * k;
+#ifdef MR_CHECKS
+  if (p.n_out) o = MR_IDX(o + k - 1, (size_t)p.n_out, 512u) - (k - 1);
+#endif
   for (int r = tid; r < k; r += kThreads) {
     p.out_keys[o + r] = fk[r];
     p.out_songs[o + r] = fs[r];
@@ -899,6 +1118,11 @@ int dev_upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t st) {
 
 using ScoreKernel = void (*)(ScoreParams);
 using NbrKernel = void (*)(NbrParams);
+using ColKernel = void (*)(ColParams);
+using PullKernel = void (*)(PullParams);
+
+// Launch shapes (mr_options.stage1 / mr_launch_info).
+enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2 };
 
 }  // namespace
 
@@ -908,14 +1132,20 @@ struct mr_ctx {
   bool loaded = false;
   bool ran = false;
   bool fused = false;
+  int shape = kShapeSeparate;
+  int te_stride = 0;  // pull: Yt row length (batch padded to 64 users)
   int last_model = -1;
   int n_tr = 0, n_te = 0, n_s = 0;
   int song_lo = 0, song_hi = 0, width = 0;
   int block_songs = 0, n_tiles = 0;
   int cap = 0, batch = 0;
-  size_t score_lds = 0, nbr_lds = 0;
+  size_t score_lds = 0, nbr_lds = 0, merge_lds = 0;
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
   NbrKernel nbr_kernel[2] = {nullptr, nullptr};
+  ColKernel col_kernel[2] = {nullptr, nullptr};
+  PullKernel pull_kernel[2] = {nullptr, nullptr};
+  DevBuf<unsigned long long> yt;
+  DevBuf<unsigned> dbg;  // MR_CHECKS builds: out-of-range index bits
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
   DevBuf<int> tr_songs, te_songs, trs_users, blk_ptr, nbr_v, nbr_cnt, cand_song, top_song;
   DevBuf<unsigned> counter;
@@ -946,6 +1176,8 @@ struct mr_ctx {
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
     dense.release();
     stamps.release();
+    yt.release();
+    dbg.release();
     loaded = ran = false;
   }
 };
@@ -989,6 +1221,17 @@ void pick_kernels(mr_ctx* c) {
   else
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
   c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
+  c->col_kernel[MODEL] = k_stage1_columns<MODEL>;
+  c->pull_kernel[MODEL] = f64 ? k_pull<MODEL, double> : k_pull<MODEL, float>;
+}
+
+// Pull shape: songs per range so that the grid has >= ~2048 workgroups
+// (4 x 64 users each), a multiple of kPullChunk.
+int pull_range(int width, int batch) {
+  const long long wy = (batch + kWaves * kPullLanes - 1) / (kWaves * kPullLanes);
+  long long r = ((long long)width * wy + 2047) / 2048;
+  r = (r + kPullChunk - 1) / kPullChunk * kPullChunk;
+  return (int)std::max<long long>(64, std::min<long long>(r, 8192));
 }
 
 }  // namespace
@@ -1024,7 +1267,7 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.out_dtype != MR_OUT_F32 && o.out_dtype != MR_OUT_F64) return fail(MR_E_INVALID, "bad out_dtype %d", o.out_dtype);
   if (o.block_songs < 0 || o.block_songs > kMaxBlockSongs || (o.block_songs % 256) != 0)
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
-  if (o.stage1 < 0 || o.stage1 > 2) return fail(MR_E_INVALID, "stage1 %d outside [0,2]", o.stage1);
+  if (o.stage1 < 0 || o.stage1 > 3) return fail(MR_E_INVALID, "stage1 %d outside [0,3]", o.stage1);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   int ndev = 0;
   MR_HIP(hipGetDeviceCount(&ndev));
@@ -1121,15 +1364,35 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const int lo = c->opt.song_lo, hi = c->opt.song_hi > 0 ? c->opt.song_hi : n_s;
   if (lo < 0 || hi > n_s || lo >= hi) return fail(MR_E_INVALID, "song shard [%d,%d) invalid for %d songs", lo, hi, n_s);
   const int width = hi - lo;
-  const bool fused = c->opt.stage1 == 1 || (c->opt.stage1 == 0 && n_tr <= kMaxFusedTrainUsers);
+  // Shape: many test users -> pull (dense Yt, gathers by song); few users and
+  // a small train set -> fused; otherwise separate.
+  const int k = c->opt.topk;
+  int shape;
+  if (c->opt.stage1 == 1) shape = kShapeFused;
+  else if (c->opt.stage1 == 2) shape = kShapeSeparate;
+  else if (c->opt.stage1 == 3) shape = kShapePull;
+  else if (n_te >= kPullMinUsers && k <= kPullMaxK) shape = kShapePull;
+  else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
+  const bool fused = shape == kShapeFused, pull = shape == kShapePull;
   if (fused && n_tr > kMaxFusedTrainUsers)
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
-  const int bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, c->opt.topk);
-  if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
-  if (c->opt.topk > 0 && bs > kMaxTopkTile)
-    return fail(MR_E_INVALID, "with topk > 0 block_songs must be <= %d (got %d)", kMaxTopkTile, bs);
+  if (pull && k > kPullMaxK) return fail(MR_E_INVALID, "pull shape keeps topk <= %d (got %d)", kPullMaxK, k);
+  // Pull: test-user batches so that Yt (n_tr x batch int64) fits 16 GiB.
+  const size_t yt_budget = (size_t)16 << 30;
+  const int pull_batch =
+      (int)std::max<size_t>(kPullLanes, std::min<size_t>((size_t)(n_te + kPullLanes - 1) / kPullLanes * kPullLanes,
+                                                         yt_budget / ((size_t)std::max(1, n_tr) * 8) / kPullLanes *
+                                                             kPullLanes));
+  int bs;
+  if (pull) {
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
+  } else {
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k);
+    if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
+    if (k > 0 && bs > kMaxTopkTile)
+      return fail(MR_E_INVALID, "with topk > 0 block_songs must be <= %d (got %d)", kMaxTopkTile, bs);
+  }
   const int n_tiles = (width + bs - 1) / bs;
-  const int k = c->opt.topk;
   // Per-song / per-user fixed-point tables, computed once on the host with
   // correctly rounded std::sqrt (java.lang.Math.sqrt semantics, MR:147/237).
   const int F = c->opt.frac_bits;
@@ -1144,8 +1407,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   for (int u = 0; u < n_te; ++u) sqrt_te[u] = std::sqrt((double)d->te_len[u]);
   // Song-tiled row pointers of the train u->s CSR: blk_ptr[v][j] = first
   // entry of S(v) with song >= min(hi, lo + j*bs).
-  std::vector<int32_t> blk_ptr((size_t)std::max(1, n_tr) * (n_tiles + 1));
-  for (int v = 0; v < n_tr; ++v) {
+  std::vector<int32_t> blk_ptr(pull ? 1 : (size_t)std::max(1, n_tr) * (n_tiles + 1));
+  for (int v = 0; v < (pull ? 0 : n_tr); ++v) {
     const int32_t* b = d->tr_songs + d->tr_off[v];
     const int32_t* e = d->tr_songs + d->tr_off[v + 1];
     for (int j = 0; j <= n_tiles; ++j) {
@@ -1156,7 +1419,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = std::max(1, n_tr);
   const size_t budget = (size_t)8 << 30;
-  const int batch = fused ? n_te : (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / ((size_t)cap * 12)));
+  const int batch = fused  ? n_te
+                    : pull ? std::min(n_te, pull_batch)
+                           : (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / ((size_t)cap * 12)));
+  const int te_stride = (batch + kPullLanes - 1) / kPullLanes * kPullLanes;
 
   hipStream_t st = c->stream;
   if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(d->tr_off), (size_t)n_tr + 1, st))) return rc;
@@ -1170,14 +1436,19 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
   if ((rc = dev_upload(c->blk_ptr, blk_ptr.data(), blk_ptr.size(), st))) return rc;
-  if (!fused) {
+  if (pull) {
+    if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
+    if ((rc = dev_alloc(c->dbg, 1))) return rc;
+    MR_HIP(hipMemsetAsync(c->dbg.p, 0, sizeof(unsigned), st));
+  } else if (!fused) {
     if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch))) return rc;
   }
   if (k > 0) {
-    if ((rc = dev_alloc(c->cand_key, (size_t)n_te * n_tiles * k))) return rc;
-    if ((rc = dev_alloc(c->cand_song, (size_t)n_te * n_tiles * k))) return rc;
+    const size_t nc = (size_t)(pull ? te_stride : n_te) * n_tiles * k;
+    if ((rc = dev_alloc(c->cand_key, nc))) return rc;
+    if ((rc = dev_alloc(c->cand_song, nc))) return rc;
     if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
     if ((rc = dev_alloc(c->top_song, (size_t)n_te * k))) return rc;
     if ((rc = dev_alloc(c->top_score, (size_t)n_te * k))) return rc;
@@ -1188,9 +1459,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_alloc(c->dense, c->opt.dense ? (size_t)n_te * width * esz : 1))) return rc;
 
   c->fused = fused;
+  c->shape = shape;
+  c->te_stride = te_stride;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
-  c->score_lds = (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles).total;
+  c->score_lds = pull ? 0 : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
                 c->score_lds);
@@ -1200,6 +1473,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
+    MR_HIP(hipFuncSetAttribute((const void*)c->col_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->nbr_lds));
+  }
+  if (pull && k > 0) {
+    c->merge_lds = (size_t)merge_lds_bytes(k);
+    MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->merge_lds));
   }
 #ifdef MR_STAMPS
   if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * kStampSlots))) return rc;
@@ -1228,7 +1508,7 @@ int mr_shard_info(const mr_ctx* c, int32_t* lo, int32_t* hi, int32_t* n_te) {
 int mr_launch_info(const mr_ctx* c, int32_t* fused, int32_t* block_songs, int32_t* n_tiles) {
   if (!c) return fail(MR_E_INVALID, "null context");
   if (!c->loaded) return fail(MR_E_STATE, "mr_launch_info before mr_load");
-  if (fused) *fused = c->fused ? 1 : 0;
+  if (fused) *fused = c->shape;
   if (block_songs) *block_songs = c->block_songs;
   if (n_tiles) *n_tiles = c->n_tiles;
   return MR_OK;
@@ -1264,16 +1544,63 @@ int run_model(mr_ctx* c, int model) {
         if (rc) return rc;
       }
       ev = &c->ring[(size_t)c->ring_used * 3];
-      c->ring_has_stage1[c->ring_used] = !c->fused;
+      c->ring_has_stage1[c->ring_used] = c->shape != kShapeFused;
       c->ring_used++;
       MR_HIP(hipEventRecord(ev[0], st));
     }
-    if (!c->fused) {
+    if (c->shape == kShapeSeparate) {
+      if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) return fail(MR_E_STATE, "separate shape without neighbour buffers");
       NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
                    c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
                    c->nbr_cnt.p};
       hipLaunchKernelGGL(c->nbr_kernel[model], dim3(nb), dim3(kThreads), c->nbr_lds, st, np);
       MR_HIP(hipGetLastError());
+    }
+    if (c->shape == kShapePull) {
+      if (!c->yt.p || (k > 0 && (!c->cand_key.p || !c->top_key.p)))
+        return fail(MR_E_STATE, "pull shape without its buffers");
+      ColParams cp{c->n_tr, user0, c->te_stride, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
+                   c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->yt.p, c->dbg.p,
+                   (long long)c->yt.n};
+      hipLaunchKernelGGL(c->col_kernel[model], dim3(nb), dim3(kThreads), c->nbr_lds, st, cp);
+      MR_HIP(hipGetLastError());
+#ifdef MR_CHECKS
+      MR_HIP(hipStreamSynchronize(st));
+#endif
+      if (timed) MR_HIP(hipEventRecord(ev[1], st));
+      PullParams pp{};
+      pp.user0 = user0; pp.n_users = nb; pp.te_stride = c->te_stride;
+      pp.song_lo = c->song_lo; pp.song_hi = c->song_hi; pp.width = c->width;
+      pp.range = c->block_songs; pp.n_ranges = c->n_tiles;
+      pp.frac_bits = c->opt.frac_bits; pp.topk = k; pp.dense = c->opt.dense;
+      pp.Yt = c->yt.p; pp.trs_off = c->trs_off.p; pp.trs_users = c->trs_users.p; pp.sqrt_c = c->sqrt_c.p;
+      pp.te_off = c->te_off.p; pp.te_songs = c->te_songs.p;
+      pp.dense_out = c->dense.p; pp.cand_key = c->cand_key.p; pp.cand_song = c->cand_song.p;
+      pp.dbg = c->dbg.p;
+      pp.n_yt = (long long)c->yt.n; pp.n_trs = (long long)c->trs_users.n; pp.n_te_songs = (long long)c->te_songs.n;
+      pp.n_te_off = (long long)c->te_off.n; pp.n_songs1 = (long long)c->trs_off.n;
+      pp.n_dense = (long long)(c->dense.n / (c->opt.out_dtype == MR_OUT_F64 ? 8 : 4));
+      pp.n_cand = (long long)c->cand_key.n;
+      const int wy = (nb + kWaves * kPullLanes - 1) / (kWaves * kPullLanes);
+      hipLaunchKernelGGL(c->pull_kernel[model], dim3(c->n_tiles, wy), dim3(kThreads), 0, st, pp);
+      MR_HIP(hipGetLastError());
+#ifdef MR_CHECKS
+      MR_HIP(hipStreamSynchronize(st));
+#endif
+      if (k > 0) {
+        MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,
+                       c->top_key.p + (size_t)user0 * k, c->top_song.p + (size_t)user0 * k,
+                       c->top_score.p + (size_t)user0 * k, c->dbg.p, (long long)c->cand_key.n,
+                       (long long)(c->top_key.n - (size_t)user0 * k)};
+        hipLaunchKernelGGL(k_topk_merge, dim3(nb), dim3(kThreads), c->merge_lds, st, mp);
+        MR_HIP(hipGetLastError());
+#ifdef MR_CHECKS
+        MR_HIP(hipStreamSynchronize(st));  // names the faulting kernel in diagnostic runs
+#endif
+      }
+      if (c->win_open) c->win_launches++;
+      if (timed) MR_HIP(hipEventRecord(ev[2], st));
+      continue;
     }
     if (timed) MR_HIP(hipEventRecord(ev[1], st));
     for (int y0 = 0; y0 < nb; y0 += 65535) {
@@ -1402,6 +1729,20 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   MR_HIP(hipGetLastError());
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
+}
+
+int mr_debug_checks(mr_ctx* c, uint32_t* bits) {
+  if (!c || !bits) return fail(MR_E_INVALID, "null argument");
+#ifndef MR_CHECKS
+  return fail(MR_E_STATE, "library built without -DMR_CHECKS");
+#else
+  *bits = 0;
+  if (!c->dbg.p) return MR_OK;
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipMemcpyAsync(bits, c->dbg.p, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  return MR_OK;
+#endif
 }
 
 int mr_debug_stamps(mr_ctx* c, int64_t* out, int64_t n) {

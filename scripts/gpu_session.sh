@@ -17,6 +17,10 @@ run() {  # name limit cmd...
   echo "== $name rc=$rc" | tee -a "$OUT/session.log"
   tail -5 "$OUT/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc in $name: stopping" | tee -a "$OUT/session.log"; exit $rc; fi
+  # a GPU memory fault surfaces as failed tests (rc 1): stop there too
+  if grep -q -E "illegal memory access|Memory access fault|HSA_STATUS_ERROR" "$OUT/$name.log"; then
+    echo "GPU fault in $name: stopping" | tee -a "$OUT/session.log"; exit 86
+  fi
   return $rc
 }
 
@@ -27,5 +31,10 @@ case ",$STEPS," in *,bench,*) run bench 600 python bench.py ;; esac
 case ",$STEPS," in *,prof,*)
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 200 ;;
+esac
+case ",$STEPS," in *,c3,*) run bench_c3 600 python bench.py --config c3 --no-cpu-baseline --steps 20 --warmup 3 ;; esac
+case ",$STEPS," in *,profc3,*)
+  export TMPDIR=/tmp
+  run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o bench -- python3 "$ROOT/bench.py" --config c3 --no-cpu-baseline --steps 20 --warmup 3 ;;
 esac
 exit 0

@@ -89,6 +89,67 @@ def test_tile_sizes_bit_identical(block, model, stage1):
     check_exact(ds, model, block_songs=block, stage1=stage1)
 
 
+# ---- pull shape (dense neighbourhoods): Yt columns + per-song row gathers ----
+@pytest.mark.parametrize("block", [256, 512, 2048, 16384])
+@pytest.mark.parametrize("model", MODELS)
+@pytest.mark.parametrize("name", ["tiny", "small"])
+def test_pull_ranges_bit_identical(name, model, block):
+    ds, z = synth_fixture(name)
+    with Engine(ds, stage1="pull", block_songs=block) as e:
+        assert e.shape == "pull" and e.block_songs == block
+    got, songs = check_exact(ds, model, stage1="pull", block_songs=block)
+    topk_consistent(songs, z[model], 10)
+
+
+@pytest.mark.parametrize("k", [1, 7, 16])
+@pytest.mark.parametrize("model", MODELS)
+def test_pull_topk_sizes(k, model):
+    ds, _ = synth_fixture("small")
+    check_exact(ds, model, k=k, stage1="pull")
+    with Engine(ds, stage1="pull", topk=k, dense=False) as e:
+        e.run(model)
+        songs, _, keys = e.topk()
+    _, ts, tk = native.fp_model(ds, model, k=k, dense=False)
+    assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
+    with Engine(ds, stage1="pull", topk=0, out_dtype="f64") as e:
+        assert np.array_equal(e.score_dense(model), native.fp_model(ds, model)[0], equal_nan=True)
+
+
+def test_pull_limits_and_kats():
+    ds, _ = synth_fixture("small")
+    with pytest.raises(_lib.EngineError):
+        Engine(ds, stage1="pull", topk=17)
+    for key in (None, "dup"):
+        K = kat() if key is None else kat()[key]
+        d = dataset_from_lines(K["train"], K["test"], K["labels"])
+        for model in MODELS:
+            got, _ = check_exact(d, model, k=4, stage1="pull")
+            assert rel_err(got, dense_from_pairs(d, K["expected"][model])) < 1e-9
+    train = ["A\ts1\t1", "A\ts2\t1", "B\ts2\t1"]
+    test = ["X\ts9\t1", "Y\ts1\t1"]
+    d = dataset_from_lines(train, test, ["X\ts1\t1"])
+    for model in MODELS:
+        _, songs = check_exact(d, model, k=3, stage1="pull")
+        assert songs[0].tolist() == [0, 1, -1]
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_pull_song_shards(model):
+    ds = synth.config("c2").dataset()
+    _, fs = check_exact(ds, model)
+    ss, kk = [], []
+    for lo, hi in song_shards(ds, 3):
+        with Engine(ds, out_dtype="f64", song_lo=lo, song_hi=hi, stage1="pull") as e:
+            e.run(model)
+            s, _, k = e.topk()
+        exp, ts, tk = native.fp_model(ds, model, song_lo=lo, song_hi=hi, k=10, dense=False)
+        assert np.array_equal(s, ts) and np.array_equal(k, tk)
+        ss.append(s)
+        kk.append(k)
+    ms, _msc, _mk = merge_topk_host(np.stack(ss), np.stack(kk))
+    assert np.array_equal(ms, fs)
+
+
 def test_launch_shape_selection():
     ds, _ = synth_fixture("small")
     with Engine(ds) as e:
@@ -127,7 +188,7 @@ def test_topk_only_mode():
     assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "pull"])
 @pytest.mark.parametrize("name", ["c1", "c2"])
 @pytest.mark.parametrize("model", MODELS)
 def test_named_configs_exact(name, model, stage1):
@@ -216,12 +277,15 @@ def test_test_user_blocks_partition():
             assert np.array_equal(e.score_dense("ibm"), full[lo:hi], equal_nan=True)
 
 
+@pytest.mark.parametrize("stage1", ["auto", "separate"])
 @pytest.mark.parametrize("model", MODELS)
-def test_c3_scale_exact_sampled_users(model):
-    """10k train / 1k test (config 3 shape): exact on a sample of test users."""
+def test_c3_scale_exact_sampled_users(model, stage1):
+    """10k train / 1k test (config 3 shape): exact on a sample of test users.
+    auto selects the pull shape here."""
     t = synth.generate(10_000, 1_000, 3, alpha=0.87)
     ds = t.dataset()
-    with Engine(ds, out_dtype="f64", topk=10) as e:
+    with Engine(ds, out_dtype="f64", topk=10, stage1=stage1) as e:
+        assert e.shape == ("pull" if stage1 == "auto" else "separate")
         e.run(model)
         dense = e.dense()
         songs, _, keys = e.topk()
