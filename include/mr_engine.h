@@ -113,7 +113,9 @@ typedef struct mr_options {
                           Yt[train user][test user] slab, the scoring kernel gathers its rows per
                           song; topk <= 16). Auto: pull from 256 test users, else fused when
                           n_train_users <= 4096, else separate. */
-  int32_t reserved[6];
+  int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
+                          to 16384, else 8192); smaller values exercise the chunked path */
+  int32_t reserved[5];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;

@@ -71,7 +71,8 @@ class MrOptions(ctypes.Structure):
         ("dense", c_int32),
         ("time_kernels", c_int32),
         ("stage1", c_int32),
-        ("reserved", c_int32 * 6),
+        ("stage1_chunk", c_int32),
+        ("reserved", c_int32 * 5),
     ]
 
 

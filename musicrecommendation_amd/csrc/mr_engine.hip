@@ -43,10 +43,13 @@ constexpr int kThreads = 256;             // 4 waves of 64
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxTopK = 64;
 constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS is 160 KiB)
-constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64)
+constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64), one chunk
+constexpr int kStage1Chunk = 8192;        // larger train sets: stage 1 in LDS chunks of train users
+constexpr int kMaxChunks = 1024;          // => n_train_users <= 8.4M
 constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live together
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
-constexpr int kMaxTopkTile = 1024;        // songs per tile when the top-k is on
+constexpr int kMaxTopkTile = 1024;        // songs per tile for the register top-k (4 per lane)
+constexpr int kMaxTopkLarge = 16;         // k limit of the wide-tile top-k (per-thread running lists)
 
 thread_local std::string g_err = "no error";
 
@@ -89,7 +92,7 @@ namespace {
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, stage_lists, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stage_lists, total;
 };
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -97,15 +100,19 @@ __host__ __device__ inline int merge_lists_per_pass(int k);
 
 // Region A (offset 0) holds the tile accumulators (+ the fused path's
 // neighbour array Y); after the tile's own top-k it is reused to stage tile
-// candidate lists for the in-launch merge (stage_lists lists per pass).
-__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles) {
+// candidate lists for the in-launch merge (stage_lists lists per pass), and
+// by the wide-tile top-k for its per-thread lists. n_chunks: separate shape's
+// stage-1 chunk count (prefix of the per-chunk neighbour counts).
+__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles, int n_chunks = 0) {
   ScoreLds L;
   const int fused = fused_ntr > 0 ? 1 : 0;
   const int kk = k > 0 ? k : 1;
   const int per = merge_lists_per_pass(kk);
   L.stage_lists = (k > 0 && n_tiles > 1) ? (n_tiles < per ? n_tiles : per) : 0;
-  const int a_bytes = bs * 8 + fused_ntr * 8;
+  int a_bytes = bs * 8 + fused_ntr * 8;
   const int st_bytes = L.stage_lists * kk * 8 + align16(L.stage_lists * kk * 4);
+  const int wide_bytes = (k > 0 && bs > kMaxTopkTile) ? kThreads * kk * 8 + kThreads * kk * 4 : 0;
+  if (wide_bytes > a_bytes) a_bytes = wide_bytes;
   int o = 0;
   L.acc = o; L.y = bs * 8; o = align16(a_bytes > st_bytes ? a_bytes : st_bytes);
   L.heard = o; o = align16(o + (bs / 32) * 4);
@@ -118,6 +125,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.fk = o; o = align16(o + kMaxTopK * 8);
   L.fs = o; o = align16(o + kMaxTopK * 4);
   L.flag = o; o = align16(o + 16);
+  L.cpre = o; o = align16(o + (n_chunks > 0 ? (n_chunks + 1) * 4 : 0));
   L.total = o;
   return L;
 }
@@ -384,6 +392,61 @@ __device__ __forceinline__ void block_topk(int n, int k, Get get, long long* wk,
   __syncthreads();
 }
 
+// Insert (key, song) into a lane's descending register list of kMaxTopkLarge
+// slots (first k used); thr tracks the k-th key (candidates at or below it
+// cannot enter, except equal keys with a lower song id, which the caller
+// excludes by visiting songs in ascending order per lane).
+__device__ __forceinline__ void lane_list_insert(long long (&tk)[kMaxTopkLarge], int (&ts)[kMaxTopkLarge], int k,
+                                                 long long key, int song, long long& thr) {
+  long long ck = key;
+  int cs = song;
+#pragma unroll
+  for (int t = 0; t < kMaxTopkLarge; ++t) {
+    const bool b = t < k && cand_before(ck, cs, tk[t], ts[t]);
+    const long long ok = tk[t];
+    const int os = ts[t];
+    tk[t] = b ? ck : tk[t];
+    ts[t] = b ? cs : ts[t];
+    ck = b ? ok : ck;
+    cs = b ? os : cs;
+  }
+  long long nt = kKeyNone;
+#pragma unroll
+  for (int t = 0; t < kMaxTopkLarge; ++t) nt = (t == k - 1) ? tk[t] : nt;
+  thr = nt;
+}
+
+// Block top-k (k <= kMaxTopkLarge) of n candidates get(i), any n: every thread
+// keeps a running list over i = tid + kThreads*j (ascending, so ties keep the
+// lower song), the 256 lists go to LDS (lk/ls: kThreads*k slots, may alias
+// the storage get() reads — a barrier separates them), each wave merges its
+// 64 lists, wave 0 merges the kWaves results. Ends with a barrier.
+template <typename Get>
+__device__ __forceinline__ void block_topk_wide(int n, int k, Get get, long long* lk, int* ls, long long* wk,
+                                                int* ws, long long* out_k, int* out_s) {
+  const int tid = threadIdx.x, w = tid >> 6;
+  long long tk[kMaxTopkLarge];
+  int ts[kMaxTopkLarge];
+#pragma unroll
+  for (int t = 0; t < kMaxTopkLarge; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
+  long long thr = kKeyNone;
+  for (int i = tid; i < n; i += kThreads) {
+    long long key;
+    int song;
+    get(i, key, song);
+    if (key > thr) lane_list_insert(tk, ts, k, key, song, thr);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kMaxTopkLarge; ++t)
+    if (t < k) { lk[tid * k + t] = tk[t]; ls[tid * k + t] = tk[t] >= 0 ? ts[t] : -1; }
+  __syncthreads();
+  wave_merge_lists(64, k, lk + (size_t)w * 64 * k, ls + (size_t)w * 64 * k, wk + w * k, ws + w * k);
+  __syncthreads();
+  if (w == 0) wave_merge_lists(kWaves, k, wk, ws, out_k, out_s);
+  __syncthreads();
+}
+
 constexpr int kMergeStageBytes = 32 * 1024;  // LDS staging of tile lists per merge pass
 __host__ __device__ inline int merge_lists_per_pass(int k) {
   const int kk = k > 0 ? k : 1;
@@ -411,8 +474,9 @@ __device__ __forceinline__ T ld_sc1(const T* p) {
 struct NbrParams {
   int n_tr;
   int user0;                 // first test user of this launch
-  int cap;                   // neighbour-list capacity per user (= n_tr)
+  int cap;                   // neighbour-list capacity per user (= n_chunks * chunk)
   int frac_bits;
+  int chunk, n_chunks;       // train users per stage-1 chunk (blockIdx.x), chunks per user
   const long long* te_off;   // [n_te+1]
   const int* te_songs;
   const long long* trs_off;  // song -> train users CSR [n_s+1]
@@ -420,28 +484,43 @@ struct NbrParams {
   const long long* q_song;   // ibm: rint(2^F / sqrt c(s))
   const double* sqrt_tr;     // sqrt(|S(v)|) with duplicates (MR:147)
   const double* sqrt_te;     // sqrt(|T(u)|) with duplicates
-  int* nbr_v;                // [batch][cap]
+  int* nbr_v;                // [batch][cap]: chunk c's list at c * chunk
   long long* nbr_q;          // [batch][cap]
-  int* nbr_cnt;              // [batch]
+  int* nbr_cnt;              // [batch][n_chunks]
 };
+
+// First index in the sorted trs_users[lo, hi) whose user is >= v.
+__device__ __forceinline__ long long lower_bound_user(const int* trs_users, long long lo, long long hi, int v) {
+  while (lo < hi) {
+    const long long m = (lo + hi) >> 1;
+    if (trs_users[m] < v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
 
 // Accumulate Y[v] += w(s2) over v ∈ L_tr(s2), s2 ∈ T(u): a flattened walk over
 // the listener lists of T(u), 256 songs of T(u) at a time; add(v, w) performs
 // the (integer, order-independent) accumulation. mark(s2) is called once per
-// song of T(u) (heard-song bookkeeping).
+// song of T(u) (heard-song bookkeeping). ranged: only listeners v in [v0, v1)
+// (a stage-1 chunk; the sorted lists are cut by binary search).
 template <int MODEL, typename Add, typename Mark>
 __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, const int* te_songs,
                                                 const long long* trs_off, const int* trs_users,
                                                 const long long* q_song, long long* s_lo, long long* s_w,
-                                                int* s_pre, int* s_scan, Add add, Mark mark) {
+                                                int* s_pre, int* s_scan, Add add, Mark mark, bool ranged = false,
+                                                int v0 = 0, int v1 = 0) {
   const int tid = threadIdx.x;
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
     int len = 0;
     if (tid < n) {
       const int s2 = te_songs[base + tid];
-      const long long lo = trs_off[s2];
-      len = (int)(trs_off[s2 + 1] - lo);
+      long long lo = trs_off[s2], hi = trs_off[s2 + 1];
+      if (ranged) {
+        lo = lower_bound_user(trs_users, lo, hi, v0);
+        hi = lower_bound_user(trs_users, lo, hi, v1);
+      }
+      len = (int)(hi - lo);
       s_lo[tid] = lo;
       s_w[tid] = (MODEL == MR_IBM) ? q_song[s2] : 1ll;
       mark(s2);
@@ -479,18 +558,21 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
   }
 }
 
+// Y indexed by v - v0 (v0 = 0 unless ranged).
 template <int MODEL>
 __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, long long t0, long long t1,
                                                       const int* te_songs, const long long* trs_off,
                                                       const int* trs_users, const long long* q_song,
                                                       long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
-                                                      unsigned* heard, int blo, int bhi) {
+                                                      unsigned* heard, int blo, int bhi, bool ranged = false,
+                                                      int v0 = 0, int v1 = 0) {
   walk_neighbours<MODEL>(
       t0, t1, te_songs, trs_off, trs_users, q_song, s_lo, s_w, s_pre, s_scan,
-      [&](int v, unsigned long long w) { atomicAdd(&Y[v], w); },
+      [&](int v, unsigned long long w) { atomicAdd(&Y[v - v0], w); },
       [&](int s2) {
         if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
-      });
+      },
+      ranged, v0, v1);
 }
 
 // Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
@@ -507,37 +589,40 @@ template <int MODEL>
 __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw);         // [n_tr]
-  long long* s_lo = reinterpret_cast<long long*>(smem_raw + align16(p.n_tr * 8));  // [256]
+  long long* s_lo = reinterpret_cast<long long*>(smem_raw + align16(p.chunk * 8));  // [256]
   long long* s_w = s_lo + kThreads;                                                // [256]
   int* s_pre = reinterpret_cast<int*>(s_w + kThreads);                             // [257]
   int* s_scan = s_pre + kThreads + 4;                                              // [kWaves]
 
-  const int bu = blockIdx.x;
+  const int c = blockIdx.x;
+  const int bu = blockIdx.y;
   const int u = p.user0 + bu;
   const int tid = threadIdx.x;
-  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+  const int cv0 = c * p.chunk, cv1 = min(p.n_tr, cv0 + p.chunk), cw = cv1 - cv0;
+  for (int i = tid; i < cw; i += kThreads) Y[i] = 0ull;
   __syncthreads();
   accumulate_neighbours<MODEL>(Y, p.te_off[u], p.te_off[u + 1], p.te_songs, p.trs_off, p.trs_users, p.q_song,
-                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0);
+                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0, p.n_chunks > 1, cv0, cv1);
 
   const double two_f = ldexp(1.0, p.frac_bits);
   const double rs_u = p.sqrt_te[u];
-  int* out_v = p.nbr_v + (size_t)bu * p.cap;
-  long long* out_q = p.nbr_q + (size_t)bu * p.cap;
+  int* out_v = p.nbr_v + (size_t)bu * p.cap + (size_t)c * p.chunk;
+  long long* out_q = p.nbr_q + (size_t)bu * p.cap + (size_t)c * p.chunk;
   int written = 0;
-  for (int v0 = 0; v0 < p.n_tr; v0 += kThreads) {
-    const int v = v0 + tid;
-    const unsigned long long y = (v < p.n_tr) ? Y[v] : 0ull;
+  for (int i0 = 0; i0 < cw; i0 += kThreads) {
+    const int i = i0 + tid;
+    const unsigned long long y = (i < cw) ? Y[i] : 0ull;
     const int flag = y != 0ull;
     int total;
     const int pos = block_excl_scan(flag, &total, s_scan);
     if (flag) {
+      const int v = cv0 + i;
       out_v[written + pos] = v;
       out_q[written + pos] = neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
     }
     written += total;
   }
-  if (tid == 0) p.nbr_cnt[bu] = written;
+  if (tid == 0) p.nbr_cnt[(size_t)bu * p.n_chunks + c] = written;
 }
 
 // ---------------------------------------------------------------------------
@@ -563,6 +648,8 @@ struct ScoreParams {
   const double* sqrt_te;
   // separate stage 1 outputs
   int cap;
+  int chunk, n_chunks;           // per-chunk neighbour lists (k_neighbours)
+  int n_users, xcd_remap;        // users of this launch; 1 = all tiles of a user on one XCD
   const int* nbr_v;
   const long long* nbr_q;
   const int* nbr_cnt;
@@ -581,7 +668,7 @@ template <int MODEL, typename OutT, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
-  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles);
+  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles, FUSED ? 0 : p.n_chunks);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
   long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
@@ -590,8 +677,18 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   int* flag = reinterpret_cast<int*>(smem_raw + L.flag);
 
-  const int tile = blockIdx.x;
-  const int bu = blockIdx.y;
+  int tile = blockIdx.x;
+  int bu = blockIdx.y;
+  if (p.xcd_remap) {
+    // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, speed
+    // only): give XCD x the users bu = 8j + x, all their tiles back to back,
+    // so a user's neighbour rows are fetched into one L2 and re-read there.
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int slot = lin >> 3;
+    bu = (slot / p.n_tiles) * 8 + (lin & 7);
+    tile = slot % p.n_tiles;
+    if (bu >= p.n_users) return;  // grid padded to a multiple of 8 users
+  }
   const int u = p.user0 + bu;
   const int tid = threadIdx.x;
   const int blo = p.song_lo + tile * bs;
@@ -673,21 +770,44 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       const int s = p.te_songs[i];
       if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
     }
+    // Prefix of the per-chunk neighbour counts: entry k of the user's
+    // flattened list lives in chunk c with cpre[c] <= k < cpre[c+1].
+    int* cpre = reinterpret_cast<int*>(smem_raw + L.cpre);
+    int* s_scan = reinterpret_cast<int*>(smem_raw + L.s_scan);
+    const int nch = p.n_chunks;
+    int cnt = 0;
+    for (int c0 = 0; c0 < nch; c0 += kThreads) {
+      const int cc = c0 + tid;
+      const int x = cc < nch ? p.nbr_cnt[(size_t)bu * nch + cc] : 0;
+      int tot;
+      const int pre = block_excl_scan(x, &tot, s_scan);
+      if (cc < nch) cpre[cc] = cnt + pre;
+      cnt += tot;
+    }
+    if (tid == 0) cpre[nch] = cnt;
+    __syncthreads();
     MR_STAMP(1);
-    const int cnt = p.nbr_cnt[bu];
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-    for (int k0 = tid; k0 < cnt; k0 += 4 * kThreads) {
-      int v[4], a[4], b[4], s0[4];
-      unsigned long long q[4];
+    constexpr int R = 8;  // neighbours per thread in flight
+    int cur = 0;          // this thread's chunk (its entries ascend)
+    for (int k0 = tid; k0 < cnt; k0 += R * kThreads) {
+      int v[R], a[R], b[R], s0[R];
+      unsigned long long q[R];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < R; ++r) {
         const int k = k0 + r * kThreads;
-        v[r] = k < cnt ? nv[k] : -1;
-        q[r] = k < cnt ? (unsigned long long)nq[k] : 0ull;
+        v[r] = -1;
+        q[r] = 0ull;
+        if (k < cnt) {
+          while (cur + 1 < nch && cpre[cur + 1] <= k) ++cur;
+          const size_t idx = (size_t)cur * p.chunk + (k - cpre[cur]);
+          v[r] = nv[idx];
+          q[r] = (unsigned long long)nq[idx];
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < R; ++r) {
         a[r] = b[r] = 0;
         if (v[r] >= 0) {
           const int* bp = p.blk_ptr + (size_t)v[r] * stride + tile;
@@ -696,9 +816,9 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
+      for (int r = 0; r < R; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < R; ++r) {
         if (s0[r] < 0) continue;
         atomicAdd(&acc[s0[r] - blo], q[r]);
         for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q[r]);
@@ -723,14 +843,19 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   __syncthreads();
   MR_STAMP(3);
 
-  // Tile top-k -> fk/fs (LDS): per-wave DPP rounds, then a 4-list tournament.
-  block_topk(
-      bw, k,
-      [&](int i, long long& key, int& song) {
-        key = (long long)acc[i];
-        song = blo + i;
-      },
-      wk, ws, fk, fs);
+  // Tile top-k -> fk/fs (LDS): per-wave DPP rounds, then a 4-list tournament;
+  // wide tiles: per-thread running lists, merged per wave, then across waves.
+  auto get_key = [&](int i, long long& key, int& song) {
+    key = (long long)acc[i];
+    song = blo + i;
+  };
+  if (bs <= kMaxTopkTile) {
+    block_topk(bw, k, get_key, wk, ws, fk, fs);
+  } else {
+    long long* lk = reinterpret_cast<long long*>(smem_raw + L.acc);
+    int* ls = reinterpret_cast<int*>(smem_raw + L.acc + kThreads * k * 8);
+    block_topk_wide(bw, k, get_key, lk, ls, wk, ws, fk, fs);
+  }
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
@@ -1139,6 +1264,7 @@ struct mr_ctx {
   int song_lo = 0, song_hi = 0, width = 0;
   int block_songs = 0, n_tiles = 0;
   int cap = 0, batch = 0;
+  int chunk = 1, n_chunks = 1;  // separate shape: stage-1 chunks of train users
   size_t score_lds = 0, nbr_lds = 0, merge_lds = 0;
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
   NbrKernel nbr_kernel[2] = {nullptr, nullptr};
@@ -1201,15 +1327,19 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
   return MR_OK;
 }
 
-int auto_block_songs(int width, int n_te, bool fused, int k) {
+int auto_block_songs(int width, int n_te, bool fused, int k, int n_tr) {
   // Aim for >= ~1024 workgroups, tiles of 256..16384 songs; with top-k a tile
   // is at most kMaxTopkTile songs (4 candidates per lane in registers); the
   // fused path keeps the neighbour array beside the tile (<= 8192).
+  // Large train sets (chunked stage 1): every tile re-walks the user's whole
+  // neighbour list, so take the widest tile (wide top-k, k <= 16).
+  long long cover = ((long long)width + 255) / 256 * 256;  // no point in a tile wider than the shard
+  if (!fused && n_tr > kMaxLdsTrainUsers && k <= kMaxTopkLarge)
+    return (int)std::max<long long>(256, std::min<long long>(kMaxBlockSongs, cover));
   const long long cap = k > 0 ? kMaxTopkTile : (fused ? 8192 : kMaxBlockSongs);
   long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
   long long bs = ((want + 255) / 256) * 256;
   bs = std::max<long long>(256, std::min<long long>(cap, bs));
-  long long cover = ((long long)width + 255) / 256 * 256;  // no point in a tile wider than the shard
   return (int)std::max<long long>(256, std::min(bs, cover));
 }
 
@@ -1269,6 +1399,8 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
   if (o.stage1 < 0 || o.stage1 > 3) return fail(MR_E_INVALID, "stage1 %d outside [0,3]", o.stage1);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
+  if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
+    return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
   int ndev = 0;
   MR_HIP(hipGetDeviceCount(&ndev));
   if (o.device < 0 || o.device >= ndev) return fail(MR_E_INVALID, "device %d not present (%d devices)", o.device, ndev);
@@ -1326,9 +1458,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const int n_tr = d->n_train_users, n_te = d->n_test_users, n_s = d->n_songs;
   if (n_tr < 0 || n_te <= 0 || n_s <= 0)
     return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d n_songs=%d", n_tr, n_te, n_s);
-  if (n_tr > kMaxLdsTrainUsers)
-    return fail(MR_E_INVALID, "n_train_users=%d exceeds the LDS stage-1 limit %d of this build", n_tr,
-                kMaxLdsTrainUsers);
+  if (n_tr > kMaxChunks * kStage1Chunk)
+    return fail(MR_E_INVALID, "n_train_users=%d exceeds the stage-1 limit %d of this build", n_tr,
+                kMaxChunks * kStage1Chunk);
   int rc;
   if ((rc = validate_csr("train user->songs", n_tr, n_s, d->tr_off, d->tr_songs))) return rc;
   if ((rc = validate_csr("test user->songs", n_te, n_s, d->te_off, d->te_songs))) return rc;
@@ -1371,12 +1503,20 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (c->opt.stage1 == 1) shape = kShapeFused;
   else if (c->opt.stage1 == 2) shape = kShapeSeparate;
   else if (c->opt.stage1 == 3) shape = kShapePull;
-  else if (n_te >= kPullMinUsers && k <= kPullMaxK) shape = kShapePull;
+  else if (n_te >= kPullMinUsers && k <= kPullMaxK && n_tr <= kMaxLdsTrainUsers) shape = kShapePull;
   else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
   const bool fused = shape == kShapeFused, pull = shape == kShapePull;
   if (fused && n_tr > kMaxFusedTrainUsers)
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
   if (pull && k > kPullMaxK) return fail(MR_E_INVALID, "pull shape keeps topk <= %d (got %d)", kPullMaxK, k);
+  if (pull && n_tr > kMaxLdsTrainUsers)
+    return fail(MR_E_INVALID, "pull shape needs n_train_users <= %d (got %d)", kMaxLdsTrainUsers, n_tr);
+  // Stage 1 of the separate shape: one LDS chunk of train users per workgroup.
+  const int chunk = c->opt.stage1_chunk > 0 ? std::min(c->opt.stage1_chunk, std::max(1, n_tr))
+                    : n_tr <= kMaxLdsTrainUsers ? std::max(1, n_tr) : kStage1Chunk;
+  if ((n_tr + chunk - 1) / chunk > kMaxChunks)
+    return fail(MR_E_INVALID, "stage1_chunk %d gives more than %d chunks", chunk, kMaxChunks);
+  const int n_chunks = (std::max(1, n_tr) + chunk - 1) / chunk;
   // Pull: test-user batches so that Yt (n_tr x batch int64) fits 16 GiB.
   const size_t yt_budget = (size_t)16 << 30;
   const int pull_batch =
@@ -1387,10 +1527,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (pull) {
     bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
   } else {
-    bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k);
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k, n_tr);
     if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
-    if (k > 0 && bs > kMaxTopkTile)
-      return fail(MR_E_INVALID, "with topk > 0 block_songs must be <= %d (got %d)", kMaxTopkTile, bs);
+    if (k > kMaxTopkLarge && bs > kMaxTopkTile)
+      return fail(MR_E_INVALID, "with topk > %d block_songs must be <= %d (got %d)", kMaxTopkLarge, kMaxTopkTile, bs);
   }
   const int n_tiles = (width + bs - 1) / bs;
   // Per-song / per-user fixed-point tables, computed once on the host with
@@ -1408,16 +1548,18 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   // Song-tiled row pointers of the train u->s CSR: blk_ptr[v][j] = first
   // entry of S(v) with song >= min(hi, lo + j*bs).
   std::vector<int32_t> blk_ptr(pull ? 1 : (size_t)std::max(1, n_tr) * (n_tiles + 1));
-  for (int v = 0; v < (pull ? 0 : n_tr); ++v) {
-    const int32_t* b = d->tr_songs + d->tr_off[v];
-    const int32_t* e = d->tr_songs + d->tr_off[v + 1];
+  for (int v = 0; v < (pull ? 0 : n_tr); ++v) {  // one merge walk over the sorted row
+    int64_t i = d->tr_off[v];
+    const int64_t e = d->tr_off[v + 1];
+    int32_t* row = blk_ptr.data() + (size_t)v * (n_tiles + 1);
     for (int j = 0; j <= n_tiles; ++j) {
       const int bound = std::min(hi, lo + j * bs);
-      blk_ptr[(size_t)v * (n_tiles + 1) + j] = (int32_t)(std::lower_bound(b, e, bound) - d->tr_songs);
+      while (i < e && d->tr_songs[i] < bound) ++i;
+      row[j] = (int32_t)i;
     }
   }
   // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
-  const int cap = std::max(1, n_tr);
+  const int cap = n_chunks * chunk;
   const size_t budget = (size_t)8 << 30;
   const int batch = fused  ? n_te
                     : pull ? std::min(n_te, pull_batch)
@@ -1443,7 +1585,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   } else if (!fused) {
     if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
-    if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch))) return rc;
+    if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
   }
   if (k > 0) {
     const size_t nc = (size_t)(pull ? te_stride : n_te) * n_tiles * k;
@@ -1463,11 +1605,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->te_stride = te_stride;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
-  c->score_lds = pull ? 0 : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles).total;
+  c->score_lds = pull ? 0 : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
                 c->score_lds);
-  c->nbr_lds = (size_t)align16(n_tr * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
+  c->nbr_lds = (size_t)align16((pull ? n_tr : chunk) * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
   for (int m = 0; m < 2; ++m) {
     MR_HIP(hipFuncSetAttribute((const void*)c->score_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
@@ -1482,8 +1624,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->merge_lds));
   }
 #ifdef MR_STAMPS
-  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * batch * kStampSlots))) return rc;
-  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * batch * kStampSlots * 8, st));
+  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * (batch + 8) * kStampSlots))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * (batch + 8) * kStampSlots * 8, st));
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
@@ -1491,6 +1633,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->song_lo = lo; c->song_hi = hi; c->width = width;
   c->block_songs = bs; c->n_tiles = n_tiles;
   c->cap = cap; c->batch = batch;
+  c->chunk = chunk; c->n_chunks = n_chunks;
   c->loaded = true;
   c->ran = false;
   return MR_OK;
@@ -1550,10 +1693,18 @@ int run_model(mr_ctx* c, int model) {
     }
     if (c->shape == kShapeSeparate) {
       if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) return fail(MR_E_STATE, "separate shape without neighbour buffers");
-      NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
-                   c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
+      NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->chunk, c->n_chunks, c->te_off.p, c->te_songs.p,
+                   c->trs_off.p, c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
                    c->nbr_cnt.p};
-      hipLaunchKernelGGL(c->nbr_kernel[model], dim3(nb), dim3(kThreads), c->nbr_lds, st, np);
+      for (int y0 = 0; y0 < nb; y0 += 65535) {
+        NbrParams q = np;
+        q.user0 = user0 + y0;
+        q.nbr_v += (size_t)y0 * c->cap;
+        q.nbr_q += (size_t)y0 * c->cap;
+        q.nbr_cnt += (size_t)y0 * c->n_chunks;
+        hipLaunchKernelGGL(c->nbr_kernel[model], dim3(c->n_chunks, std::min(65535, nb - y0)), dim3(kThreads),
+                           c->nbr_lds, st, q);
+      }
       MR_HIP(hipGetLastError());
     }
     if (c->shape == kShapePull) {
@@ -1603,9 +1754,14 @@ int run_model(mr_ctx* c, int model) {
       continue;
     }
     if (timed) MR_HIP(hipEventRecord(ev[1], st));
-    for (int y0 = 0; y0 < nb; y0 += 65535) {
-      const int ny = std::min(65535, nb - y0);
+    for (int y0 = 0; y0 < nb; y0 += 65528) {
+      const int ny = std::min(65528, nb - y0);
+      // separate shape: all tiles of a user on one XCD (grid padded to 8 users)
+      const int remap = c->shape == kShapeSeparate && c->n_tiles > 1;
+      const int gy = remap ? (ny + 7) / 8 * 8 : ny;
       ScoreParams sp{};
+      sp.chunk = c->chunk; sp.n_chunks = c->n_chunks;
+      sp.n_users = ny; sp.xcd_remap = remap;
       sp.n_tr = c->n_tr;
       sp.user0 = user0 + y0;
       sp.song_lo = c->song_lo; sp.song_hi = c->song_hi; sp.width = c->width;
@@ -1618,12 +1774,12 @@ int run_model(mr_ctx* c, int model) {
       sp.cap = c->cap;
       sp.nbr_v = c->fused ? nullptr : c->nbr_v.p + (size_t)y0 * c->cap;
       sp.nbr_q = c->fused ? nullptr : c->nbr_q.p + (size_t)y0 * c->cap;
-      sp.nbr_cnt = c->fused ? nullptr : c->nbr_cnt.p + y0;
+      sp.nbr_cnt = c->fused ? nullptr : c->nbr_cnt.p + (size_t)y0 * c->n_chunks;
       sp.dense_out = c->dense.p;
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
-      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, ny), dim3(kThreads), c->score_lds, st, sp);
+      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(kThreads), c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
       if (c->win_open) c->win_launches++;
     }

@@ -138,3 +138,80 @@ def config(name: str, n_test: Optional[int] = None) -> Triplets:
     if alpha is None and target is not None:
         alpha = calibrate_alpha(n_tr, n_te, seed, target)
     return generate(n_tr, n_test if n_test is not None else n_te, seed, alpha=alpha)
+
+
+# ---------------------------------------------------------------------------
+# Full-scale generator (C4/C5: ~1M users, ~48M rows). Same distributions as
+# ``generate`` but drawn in bulk with numpy (one RNG stream per call, so it is
+# NOT prefix-consistent with ``generate``) and with the popularity head capped
+# (pure Zipf(0.87) would give the top song more listeners than
+# users; the cap keeps every song's expected listener share <= head_cap).
+# ---------------------------------------------------------------------------
+def capped_popularity(alpha: float, n_universe: int, mean_len: float, head_cap: float) -> np.ndarray:
+    """Zipf(alpha) probabilities with water-filling: no song's expected share of
+    users (p * mean_len) exceeds head_cap; the excess is spread over the tail."""
+    p = np.arange(1, n_universe + 1, dtype=np.float64) ** (-alpha)
+    p /= p.sum()
+    p_max = head_cap / mean_len
+    for _ in range(200):
+        over = p > p_max
+        if not over.any():
+            break
+        excess = float((p[over] - p_max).sum())
+        p[over] = p_max
+        free = ~over & (p < p_max)
+        p[free] += excess * p[free] / p[free].sum()
+    return p
+
+
+def generate_bulk(n_train: int, n_test: int, seed: int, alpha: float = 0.87,
+                  head_cap: float = 0.10, n_universe: int = N_SONG_UNIVERSE) -> Triplets:
+    """Bulk draw of n_train + n_test users (train first, then test), history
+    lengths max(10, round(lognormal(3.51, 0.86))), distinct songs by capped
+    Zipf popularity in draw order; test users split ceil(n/2) visible / rest
+    labels (NB:571-573)."""
+    rng = np.random.default_rng([seed, 7])
+    n_users = n_train + n_test
+    lens = np.maximum(10, np.rint(rng.lognormal(3.51, 0.86, n_users))).astype(np.int64)
+    lens = np.minimum(lens, n_universe)
+    p = capped_popularity(alpha, n_universe, float(lens.mean()), head_cap)
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    perm = np.random.default_rng([seed, 0]).permutation(n_universe).astype(np.int64)
+    # rounds of oversampled draws for the users still short of their length
+    got_u = np.zeros(0, np.int64)
+    got_s = np.zeros(0, np.int64)
+    got_o = np.zeros(0, np.int64)  # global draw order
+    have = np.zeros(n_users, np.int64)
+    order0 = 0
+    for _ in range(64):
+        need = lens - have
+        short = np.nonzero(need > 0)[0]
+        if short.size == 0:
+            break
+        m = (need[short] * 5) // 4 + 8
+        u = np.repeat(short, m)
+        r = np.searchsorted(cdf, rng.random(u.size), side="right")
+        s = perm[np.minimum(r, n_universe - 1)]
+        o = order0 + np.arange(u.size, dtype=np.int64)
+        order0 += u.size
+        u = np.concatenate([got_u, u]); s = np.concatenate([got_s, s]); o = np.concatenate([got_o, o])
+        key = u * n_universe + s
+        _, first = np.unique(key, return_index=True)       # first draw of each (user, song)
+        u, s, o = u[first], s[first], o[first]
+        idx = np.lexsort((o, u))                           # per user, in draw order
+        u, s, o = u[idx], s[idx], o[idx]
+        start = np.searchsorted(u, np.arange(n_users))
+        rank = np.arange(u.size) - start[u]
+        keep = rank < lens[u]
+        got_u, got_s, got_o = u[keep], s[keep], o[keep]
+        have = np.bincount(got_u, minlength=n_users)
+    else:
+        raise RuntimeError("bulk synthetic draw did not converge")
+    start = np.searchsorted(got_u, np.arange(n_users))
+    rank = np.arange(got_u.size) - start[got_u]
+    is_tr = got_u < n_train
+    vis = rank < (lens[got_u] + 1) // 2
+    te = ~is_tr & vis
+    lb = ~is_tr & ~vis
+    return Triplets(got_u[is_tr], got_s[is_tr], got_u[te], got_s[te], got_u[lb], got_s[lb], float(alpha))

@@ -75,9 +75,9 @@ def test_golden_fixture(name, model):
 @pytest.mark.parametrize("model", MODELS)
 def test_tile_sizes_bit_identical(block, model, stage1):
     ds, _ = synth_fixture("small")
-    if block > 1024:  # top-k tiles hold <= 1024 songs; dense-only tiles may be larger
+    if block > 1024:  # wide tiles: per-thread running top-k lists, k <= 16
         with pytest.raises(_lib.EngineError):
-            Engine(ds, block_songs=block, stage1=stage1)
+            Engine(ds, block_songs=block, stage1=stage1, topk=17)
         if stage1 == "fused" and block > 8192:
             with pytest.raises(_lib.EngineError):
                 Engine(ds, block_songs=block, stage1=stage1, topk=0)
@@ -85,8 +85,56 @@ def test_tile_sizes_bit_identical(block, model, stage1):
         with Engine(ds, block_songs=block, stage1=stage1, topk=0, out_dtype="f64") as e:
             got = e.score_dense(model)
         assert np.array_equal(got, native.fp_model(ds, model)[0], equal_nan=True)
-        return
     check_exact(ds, model, block_songs=block, stage1=stage1)
+
+
+# ---- chunked stage 1 / wide tiles (large train sets, config 4 shape) -------
+@pytest.mark.parametrize("chunk", [1, 3, 7, 64])
+@pytest.mark.parametrize("model", MODELS)
+@pytest.mark.parametrize("name", ["tiny", "small", "kat"])
+def test_stage1_chunks_bit_identical(name, model, chunk):
+    if name == "kat":
+        K = kat()
+        ds = dataset_from_lines(K["train"], K["test"], K["labels"])
+    else:
+        ds, _ = synth_fixture(name)
+    check_exact(ds, model, k=4, stage1="separate", stage1_chunk=chunk)
+    check_exact(ds, model, k=4, stage1="separate", stage1_chunk=chunk, block_songs=256)
+
+
+@pytest.mark.parametrize("k", [1, 10, 16])
+@pytest.mark.parametrize("block", [2048, 4096, 16384])
+@pytest.mark.parametrize("model", MODELS)
+def test_wide_tiles_c2(block, model, k):
+    ds = synth.config("c2", n_test=13).dataset()
+    check_exact(ds, model, k=k, stage1="separate", block_songs=block)
+    if block <= 8192:
+        check_exact(ds, model, k=k, stage1="fused", block_songs=block)
+
+
+@pytest.mark.parametrize("model", MODELS)
+def test_large_train_set_exact(model):
+    """n_train > 16384: chunked stage 1 (8192 train users per LDS chunk),
+    16384-song tiles, XCD-grouped tiles; every user exact vs the oracle."""
+    ds = synth.generate_bulk(40_000, 21, 4).dataset()
+    with Engine(ds, out_dtype="f64", topk=10) as e:
+        assert e.shape == "separate" and e.block_songs == 16384
+        e.run(model)
+        dense = e.dense()
+        songs, _, keys = e.topk()
+    exp, ts, tk = native.fp_model(ds, model, k=10)
+    assert np.array_equal(dense, exp, equal_nan=True)
+    assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
+    # song shards of the large set: merged lists identical
+    ss, kk = [], []
+    for lo, hi in song_shards(ds, 3):
+        with Engine(ds, song_lo=lo, song_hi=hi, topk=10, dense=False) as e:
+            e.run(model)
+            s, _, k = e.topk()
+        ss.append(s)
+        kk.append(k)
+    ms, _msc, mk = merge_topk_host(np.stack(ss), np.stack(kk))
+    assert np.array_equal(ms, ts) and np.array_equal(mk, tk)
 
 
 # ---- pull shape (dense neighbourhoods): Yt columns + per-song row gathers ----
