@@ -56,11 +56,18 @@ def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
     trs_users = np.repeat(np.arange(ds.n_train), tr_deg)[order]
     c_tr = np.diff(trs_ptr)
     b1 = b2 = 0
+    mark = np.zeros(ds.n_train, dtype=bool)
     for u in range(ds.n_test):
         T = ds.te_songs[ds.te_off[u]:ds.te_off[u + 1]]
-        nb = np.unique(np.concatenate([trs_users[trs_ptr[s]:trs_ptr[s + 1]] for s in T])) if T.size else []
+        if T.size:
+            flat = np.concatenate([trs_users[trs_ptr[s]:trs_ptr[s + 1]] for s in T])
+            mark[flat] = True
+            nb = np.flatnonzero(mark)
+            mark[flat] = False
+        else:
+            nb = np.zeros(0, dtype=np.int64)
         b1 += 12 * T.size + 4 * int(c_tr[T].sum())
-        b2 += int(np.sum(8 + 4 * tr_deg[nb])) + 4 * n_s + out_bytes * (n_s - T.size)
+        b2 += int(nb.size) * 8 + 4 * int(tr_deg[nb].sum()) + 4 * n_s + out_bytes * (n_s - T.size)
     return {"neighbours": b1, "score": b2, "merge": 12 * k * ds.n_test}
 
 
@@ -98,6 +105,36 @@ def cpu_baseline(ds, model: str, seconds: float):
     }
 
 
+def cpu_baseline_twohop(ds, model: str, seconds: float):
+    """Full-scale configs: the literal string-id loop nest is infeasible (SURVEY.md
+    §8d), so time the CPU two-hop restatement (oracle/fixedpoint.c, one thread,
+    top-k only) on the first test users, bounded to ~`seconds`."""
+    from oracle import native
+
+    def pairs(n):
+        return n * ds.n_songs - int(ds.te_off[n])
+
+    # Each call re-transposes the train CSR (a fixed cost the reference's
+    # timed region does not contain): rate = difference of two user counts.
+    prev = (0, 0.0)
+    n = 1
+    while True:
+        t0 = time.perf_counter()
+        native.fp_model(ds, model, user_lo=0, user_hi=n, k=10, dense=False)
+        dt = time.perf_counter() - t0
+        if (dt > seconds / 3 and prev[0] > 0) or n >= ds.n_test:
+            break
+        prev = (n, dt)
+        n = min(ds.n_test, n * 2)
+    dp, dtt = pairs(n) - pairs(prev[0]), max(dt - prev[1], 1e-9)
+    return {
+        "value": dp / dtt, "unit": "pairs/s", "cores": 1, "kind": "port",
+        "sample": f"oracle/fixedpoint.c {model} two-hop (int64 fixed point, top-10 only): test users "
+                  f"{prev[0]}..{n} of {ds.n_test} ({dp} pairs) in {dtt:.1f} s (difference of two runs, "
+                  f"so the per-call train transpose is excluded)",
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,8 +161,30 @@ def main() -> None:
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    n_tr, n_te, _seed, _t = synth.CONFIGS[args.config]
-    if args.shard == "users":
+    bulk = args.config in synth.BULK_CONFIGS
+    if bulk:  # full-scale: fixed test set, top-k only (SURVEY.md §8d OUT = 12k)
+        n_tr, n_te, _seed = synth.BULK_CONFIGS[args.config]
+    else:
+        n_tr, n_te, _seed, _t = synth.CONFIGS[args.config]
+    dense_out = not bulk
+    if args.shard == "users" and bulk:
+        # strong scaling: rank r scores test users [n_te r / N, n_te (r+1) / N)
+        full = synth.config(args.config).dataset()
+        lo, hi = n_te * rank // world, n_te * (rank + 1) // world
+        blocks = [full.subset_test_users(lo, hi)]
+        engines = [Engine(blocks[0], device=local, out_dtype="f32", topk=10, dense=False)]
+        ds = blocks[0]
+        eng = engines[0]
+        pairs_per_engine = [blocks[0].n_pairs()]
+        step_i = [0]
+
+        def step():
+            engines[0].run(args.model)
+            step_i[0] += 1
+
+        def drain():
+            engines[0].sync()
+    elif args.shard == "users":
         # rank r, in-flight slot j scores test-user block (r * inflight + j) of a
         # 500 x (10 * world * inflight) dataset: disjoint blocks, same train set
         nb = world * args.inflight
@@ -149,8 +208,8 @@ def main() -> None:
     else:
         from musicrecommendation_amd.sharding import SongShardScorer
 
-        full = ds = synth.config(args.config, n_test=n_te * world).dataset()
-        scorer = SongShardScorer(ds, rank, world, local, topk=10, out_dtype="f32")
+        full = ds = synth.config(args.config, n_test=None if bulk else n_te * world).dataset()
+        scorer = SongShardScorer(ds, rank, world, local, topk=10, out_dtype="f32", dense=dense_out)
         eng = scorer.engine
         heard = ds.heard_mask()[:, eng.song_lo:eng.song_hi]
         pairs_rank = int(heard.size - heard.sum())
@@ -195,7 +254,7 @@ def main() -> None:
 
     if rank == 0:
         value = pairs_all / elapsed_max
-        ab_stage = algorithmic_bytes(ds, 4, 10)
+        ab_stage = algorithmic_bytes(ds, 4 if dense_out else 0, 10)
         if eng.fused:
             # one kernel per step: the window's mean is that kernel's mean launch
             # duration (plus the launch gaps, which the rocprof summary excludes)
@@ -204,7 +263,11 @@ def main() -> None:
         else:
             dom = "steps"
             ab_dom = sum(ab_stage.values())
-        avg_us = win_ms / max(n_launch, 1) * 1e3
+        # the launches of one step run back to back on the engine stream: the
+        # window over K steps / K is the step's device time (= the fused
+        # kernel's launch time at C2; all of a step's kernels otherwise)
+        avg_us = win_ms / max(args.steps, 1) * 1e3
+        launches_per_step = n_launch / max(args.steps, 1)
         achieved = ab_dom / (avg_us * 1e-6) / 1e9
         step_bytes = sum(ab_stage.values())
         traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
@@ -220,7 +283,7 @@ def main() -> None:
         if args.shard == "users":
             songs, _sc, _k = eng.topk()
             map10 = evaluation.map_at_k(songs, ds, 10)
-            ref_map = evaluation.threshold_map(eng.dense().astype(np.float64), ds)
+            ref_map = evaluation.threshold_map(eng.dense().astype(np.float64), ds) if dense_out else None
         else:
             s_, _k = scorer.topk()
             map10 = evaluation.map_at_k(s_, ds, 10)
@@ -235,14 +298,15 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if bulk else "weak",
             "vs_baseline": value / SCALA_PAR_PAIRS_PER_S if args.model == "ibm" else None,
             "dtype": "int64",
             "data": "synthetic (seeded Zipf/lognormal Taste-Profile-shaped triplets, SURVEY.md §8d)",
             "config": {
                 "workload": f"{args.config}: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} "
-                            f"{n_tr} train / {n_te} test per GPU / {full.n_songs} songs, "
-                            f"fp32 dense scores + top-10, shard={args.shard}",
+                            f"{n_tr} train / {n_te} test {'in total' if bulk else 'per GPU'} / "
+                            f"{full.n_songs} songs, {'fp32 dense scores + ' if dense_out else ''}top-10, "
+                            f"shard={args.shard}",
                 "n_train": n_tr, "n_test": full.n_test, "n_songs": full.n_songs,
                 "pairs_per_step": pairs_all / args.steps, "parallelism": f"{args.shard}{world}",
                 "inflight": args.inflight,
@@ -251,7 +315,8 @@ def main() -> None:
                 "bound": "hbm",
                 "kernel": {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
                            "separate": "k_neighbours + k_score (per step)",
-                           "pull": "k_stage1_columns + k_pull + k_topk_merge (per step)"}[eng.shape],
+                           "pull": "k_stage1_columns + k_pull + k_topk_merge (per step)",
+                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)"}[eng.shape],
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -260,8 +325,9 @@ def main() -> None:
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": ab_dom,
                 "avg_launch_us": avg_us,
+                "launches_per_step": launches_per_step,
                 "timing": f"HIP events on the engine stream around the {args.steps} timed steps "
-                          f"({n_launch} scoring launches)",
+                          f"({n_launch} scoring launches; avg_launch_us = device time per step)",
             },
             "launch": {"shape": eng.shape, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles},
             "step_algorithmic_bytes": step_bytes,
@@ -270,7 +336,8 @@ def main() -> None:
             "ref_threshold_mAP": ref_map,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(ds, args.model, args.cpu_baseline_seconds)
+            line["cpu_baseline"] = (cpu_baseline_twohop(ds, args.model, args.cpu_baseline_seconds) if bulk
+                                    else cpu_baseline(ds, args.model, args.cpu_baseline_seconds))
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

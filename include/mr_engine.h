@@ -111,7 +111,10 @@ typedef struct mr_options {
                           song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel
                           (compact neighbour lists), 3 = pull (stage 1 writes a dense
                           Yt[train user][test user] slab, the scoring kernel gathers its rows per
-                          song; topk <= 16). Auto: pull from 256 test users, else fused when
+                          song; topk <= 16), 4 = wide (large train sets: chunked stage 1, 16k-song
+                          tiles scored by 1024-thread workgroups, separate top-k merge launch;
+                          topk <= 16). Auto: pull from 256 test users (n_train_users <= 16384),
+                          else wide when n_train_users > 16384, else fused when
                           n_train_users <= 4096, else separate. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
                           to 16384, else 8192); smaller values exercise the chunked path */
@@ -134,7 +137,7 @@ int mr_load(mr_ctx* ctx, const mr_dataset* d);
  * test users. The dense model of this context is n_te x (song_hi - song_lo). */
 int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
 
-/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull; songs
+/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull, 3 wide; songs
  * per LDS tile (pull: per song range) and tiles (ranges) per test user. */
 int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int32_t* n_tiles);
 

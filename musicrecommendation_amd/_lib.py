@@ -18,8 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MR_ENGINE_LIB=stamps|checks selects a diagnostic build (phase timestamps /
 # bounds-checked pull kernels).
 _VARIANT = os.environ.get("MR_ENGINE_LIB", "")
-LIB_PATH = os.path.join(_HERE, f"libmr_engine_{_VARIANT}.so" if _VARIANT in ("stamps", "checks")
-                        else "libmr_engine.so")
+LIB_PATH = os.path.join(_HERE, f"libmr_engine_{_VARIANT}.so" if _VARIANT else "libmr_engine.so")
 
 MR_OK = 0
 MR_E_INVALID = -1

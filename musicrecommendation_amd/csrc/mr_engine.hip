@@ -37,6 +37,7 @@
 
 #include "mr_engine.h"
 
+
 namespace {
 
 constexpr int kThreads = 256;             // 4 waves of 64
@@ -92,8 +93,13 @@ namespace {
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stage_lists, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, stage_lists, total;
 };
+
+// Separate shape, stage 2: per-wave staging of one round of neighbours
+// (kStgItems segments: start, exclusive prefix of lengths, weight).
+constexpr int kStgItems = 256;
+constexpr int kStgBytes = kStgItems * 8 + kStgItems * 4 + (kStgItems + 4) * 4;  // q, a, pre
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 __host__ __device__ inline int merge_lists_per_pass(int k);
@@ -126,6 +132,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.fs = o; o = align16(o + kMaxTopK * 4);
   L.flag = o; o = align16(o + 16);
   L.cpre = o; o = align16(o + (n_chunks > 0 ? (n_chunks + 1) * 4 : 0));
+  L.stg = o; o = align16(o + (n_chunks > 0 ? kWaves * kStgBytes : 0));
   L.total = o;
   return L;
 }
@@ -454,6 +461,14 @@ __host__ __device__ inline int merge_lists_per_pass(int k) {
   return l > 256 ? 256 : (l < 2 ? 2 : l);
 }
 
+// Wave-private LDS hand-off: wait for this wave's LDS ops, keep the compiler
+// from reordering across it (a single wave needs no s_barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // sc1 (L2-coherent, agent-scope) stores/loads for the in-launch hand-off of
 // tile candidates to the user's last workgroup (MI355X_MICROARCH.md, "Valid
 // forms", row 1: sc1 stores, vmcnt(0), barrier, one agent atomic add per
@@ -637,8 +652,9 @@ struct ScoreParams {
   int frac_bits, topk, dense;
   const long long* te_off;
   const int* te_songs;
-  const int* tr_songs;           // train u -> s column ids
-  const int* blk_ptr;            // [n_tr][n_tiles+1] index into tr_songs
+  const int* toff;               // tile-major train CSR: [n_tiles * n_tr + 1]; tile t, user v ->
+                                 //   tsongs[toff[t*n_tr+v] .. toff[t*n_tr+v+1])
+  const unsigned short* tsongs;  // tile-local song ids (s - tile start), rows sorted
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
   // fused stage 1 inputs
   const long long* trs_off;
@@ -694,7 +710,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   const int blo = p.song_lo + tile * bs;
   const int bhi = min(p.song_hi, blo + bs);
   const int bw = bhi - blo;
-  const int stride = p.n_tiles + 1;
   const double two_f = ldexp(1.0, p.frac_bits);
 #ifdef MR_STAMPS
   long long* sb = p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr;
@@ -716,7 +731,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       const int v = tid + r * kThreads;
       pa[r] = pb[r] = 0;
       if (v < p.n_tr) {
-        const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+        const int* bp = p.toff + (size_t)tile * p.n_tr + v;
         pa[r] = bp[0];
         pb[r] = bp[1];
       }
@@ -746,22 +761,22 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
             a[r] = pa[r];
             b[r] = pb[r];
           } else {
-            const int* bp = p.blk_ptr + (size_t)v * stride + tile;
+            const int* bp = p.toff + (size_t)tile * p.n_tr + v;
             a[r] = bp[0];
             b[r] = bp[1];
           }
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
+      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? (int)p.tsongs[a[r]] : -1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (s0[r] < 0) continue;
         const int v = v0 + r * kThreads;
         const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
             y[r], rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
-        atomicAdd(&acc[s0[r] - blo], q);
-        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q);
+        atomicAdd(&acc[s0[r]], q);
+        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tsongs[x]], q);
       }
     }
   } else {
@@ -789,14 +804,28 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     MR_STAMP(1);
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-    constexpr int R = 8;  // neighbours per thread in flight
-    int cur = 0;          // this thread's chunk (its entries ascend)
-    for (int k0 = tid; k0 < cnt; k0 += R * kThreads) {
-      int v[R], a[R], b[R], s0[R];
-      unsigned long long q[R];
+    // Load-balanced scatter: each wave takes rounds of kStgItems neighbours
+    // (R per lane), stages their tile segments (start, length prefix, weight)
+    // in LDS, then its lanes walk the round's flattened entries, E per lane in
+    // flight — segment lengths are heavy-tailed (heavy listeners dominate
+    // N(u)), so per-lane segment loops would leave the wave waiting on its
+    // longest segment.
+    const int lane = tid & 63, w = tid >> 6;
+    unsigned char* stg = smem_raw + L.stg + w * kStgBytes;
+    unsigned long long* st_q = reinterpret_cast<unsigned long long*>(stg);
+    int* st_a = reinterpret_cast<int*>(stg + kStgItems * 8);
+    int* st_pre = st_a + kStgItems;
+    constexpr int R = kStgItems / 64;
+    constexpr int E = 16;
+    const int* toff_t = p.toff + (size_t)tile * p.n_tr;
+    // Software pipeline over rounds (one wave): round i is scattered while the
+    // row offsets of round i+1 and the list entries of round i+2 are in
+    // flight, so one memory latency covers three dependent levels.
+    int cur = 0;  // this lane's chunk (its items ascend)
+    auto load_list = [&](int k0, int (&v)[R], unsigned long long (&q)[R]) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int k = k0 + r * kThreads;
+        const int k = k0 + r * 64 + lane;
         v[r] = -1;
         q[r] = 0ull;
         if (k < cnt) {
@@ -806,22 +835,72 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
           q[r] = (unsigned long long)nq[idx];
         }
       }
+    };
+    auto load_offsets = [&](const int (&v)[R], int (&a)[R], int (&b)[R]) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         a[r] = b[r] = 0;
         if (v[r] >= 0) {
-          const int* bp = p.blk_ptr + (size_t)v[r] * stride + tile;
-          a[r] = bp[0];
-          b[r] = bp[1];
+          a[r] = toff_t[v[r]];
+          b[r] = toff_t[v[r] + 1];
         }
       }
-#pragma unroll
-      for (int r = 0; r < R; ++r) s0[r] = a[r] < b[r] ? p.tr_songs[a[r]] : -1;
+    };
+    const int step = kWaves * kStgItems;
+    int v0[R], a0[R], b0[R], v1[R], a1[R], b1[R], v2[R];
+    unsigned long long q0[R], q1[R], q2[R];
+    int k0 = w * kStgItems;
+    load_list(k0, v0, q0);
+    load_offsets(v0, a0, b0);
+    load_list(k0 + step, v1, q1);
+    for (; k0 < cnt; k0 += step) {
+      int run = 0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (s0[r] < 0) continue;
-        atomicAdd(&acc[s0[r] - blo], q[r]);
-        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tr_songs[x] - blo], q[r]);
+        const int len = b0[r] - a0[r];
+        int incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int y = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += y;
+        }
+        const int it = r * 64 + lane;
+        st_a[it] = a0[r];
+        st_pre[it] = run + incl - len;
+        st_q[it] = q0[r];
+        run += __shfl(incl, 63, 64);
+      }
+      if (lane == 0) st_pre[kStgItems] = run;
+      wave_lds_sync();
+      load_offsets(v1, a1, b1);            // round i+1
+      load_list(k0 + 2 * step, v2, q2);    // round i+2
+      for (int j0 = 0; j0 < run; j0 += 64 * E) {
+        int song[E], it[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int j = j0 + e * 64 + lane;
+          song[e] = -1;
+          it[e] = 0;
+          if (j < run) {
+            int lo = 0, hi = kStgItems;  // last item with st_pre[item] <= j
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+              const int m = (lo + hi) >> 1;
+              if (st_pre[m] <= j) lo = m; else hi = m;
+            }
+            song[e] = (int)p.tsongs[st_a[lo] + (j - st_pre[lo])];
+            it[e] = lo;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (song[e] >= 0) atomicAdd(&acc[song[e]], st_q[it[e]]);
+      }
+      wave_lds_sync();  // the next round overwrites the staging
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a0[r] = a1[r]; b0[r] = b1[r]; q0[r] = q1[r];
+        v1[r] = v2[r]; q1[r] = q2[r];
       }
     }
   }
@@ -946,6 +1025,211 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// wide shape (large train sets, config 4): one (test user, 16k-song tile)
+// per NT-thread workgroup. The 128 KiB tile admits one workgroup per CU, so
+// the workgroup itself is wide (NT = 1024: 4 waves per SIMD) to keep enough
+// independent neighbour visits in flight; the per-(v, tile) segments are
+// short (|S(v)| / n_tiles), heavy-tailed work is spread by the hardware over
+// 16 waves. Tile candidates go to cand_key/cand_song; k_topk_merge reduces
+// them per user in a second launch. MR:159-166 / MR:249-257.
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ int block_excl_scan_nt(int x, int* total, int* sbuf) {
+  constexpr int NW = NT / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) sbuf[w] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int v = sbuf[i];
+    off += (i < w) ? v : 0;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + incl - x;
+}
+
+template <int NT>
+struct WideLds {
+  int acc, heard, cpre, s_scan, wk, ws, fk, fs, total;
+};
+template <int NT>
+__host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
+  constexpr int NW = NT / 64;
+  const int kk = k > 0 ? k : 1;
+  WideLds<NT> L;
+  int o = 0;
+  L.acc = o; o = align16(o + bs * 8);
+  L.heard = o; o = align16(o + (bs / 32) * 4);
+  L.cpre = o; o = align16(o + (n_chunks + 1) * 4);
+  L.s_scan = o; o = align16(o + NW * 4);
+  L.wk = o; o = align16(o + NW * kk * 8);
+  L.ws = o; o = align16(o + NW * kk * 4);
+  L.fk = o; o = align16(o + kk * 8);
+  L.fs = o; o = align16(o + kk * 4);
+  L.total = o;
+  return L;
+}
+
+constexpr int kWideThreads = 1024;
+
+template <int MODEL, typename OutT, int NT>
+__global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
+  constexpr int NW = NT / 64;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int bs = p.block_songs;
+  const WideLds<NT> L = wide_lds<NT>(bs, p.topk, p.n_chunks);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
+  unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
+  int* cpre = reinterpret_cast<int*>(smem_raw + L.cpre);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + L.s_scan);
+
+  // all tiles of a user on one XCD (round-robin dealing, speed only)
+  const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+  const int slot = lin >> 3;
+  const int bu = (slot / p.n_tiles) * 8 + (lin & 7);
+  const int tile = slot % p.n_tiles;
+  if (bu >= p.n_users) return;  // grid padded to a multiple of 8 users
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int blo = p.song_lo + tile * bs;
+  const int bhi = min(p.song_hi, blo + bs);
+  const int bw = bhi - blo;
+  MR_STAMP(0);
+
+  for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
+  for (int i = tid; i < bs / 32; i += NT) heard[i] = 0u;
+  __syncthreads();
+  for (long long i = p.te_off[u] + tid; i < p.te_off[u + 1]; i += NT) {
+    const int s = p.te_songs[i];
+    if (s >= blo && s < bhi) atomicOr(&heard[(s - blo) >> 5], 1u << ((s - blo) & 31));
+  }
+  const int nch = p.n_chunks;
+  int cnt = 0;
+  for (int c0 = 0; c0 < nch; c0 += NT) {
+    const int cc = c0 + tid;
+    const int x = cc < nch ? p.nbr_cnt[(size_t)bu * nch + cc] : 0;
+    int tot;
+    const int pre = block_excl_scan_nt<NT>(x, &tot, s_scan);
+    if (cc < nch) cpre[cc] = cnt + pre;
+    cnt += tot;
+  }
+  if (tid == 0) cpre[nch] = cnt;
+  __syncthreads();
+  MR_STAMP(1);
+
+  // stage 2: R neighbours per thread in flight; each segment's first kSeg
+  // entries are loaded in the same batch, longer tails loop.
+  {
+    const int* nv = p.nbr_v + (size_t)bu * p.cap;
+    const long long* nq = p.nbr_q + (size_t)bu * p.cap;
+    const int* toff_t = p.toff + (size_t)tile * p.n_tr;
+    constexpr int R = 2, kSeg = 4;
+    int cur = 0;
+    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
+      int v[R], a[R], b[R];
+      unsigned long long q[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = k0 + r * NT;
+        v[r] = -1;
+        q[r] = 0ull;
+        if (k < cnt) {
+          while (cur + 1 < nch && cpre[cur + 1] <= k) ++cur;
+          const size_t idx = (size_t)cur * p.chunk + (k - cpre[cur]);
+          v[r] = nv[idx];
+          q[r] = (unsigned long long)nq[idx];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a[r] = b[r] = 0;
+        if (v[r] >= 0) {
+          a[r] = toff_t[v[r]];
+          b[r] = toff_t[v[r] + 1];
+        }
+      }
+      int sg[R][kSeg];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) sg[r][j] = a[r] + j < b[r] ? (int)p.tsongs[a[r] + j] : -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j)
+          if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q[r]);
+        for (int x = a[r] + kSeg; x < b[r]; ++x) atomicAdd(&acc[p.tsongs[x]], q[r]);
+      }
+    }
+  }
+  __syncthreads();
+  MR_STAMP(2);
+
+  // epilogue: scores -> dense row segment; keys back into acc
+  const double inv_f = ldexp(1.0, -p.frac_bits);
+  OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
+  for (int i = tid; i < bw; i += NT) {
+    const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+    double score = (double)(long long)acc[i] * inv_f;
+    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
+    if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+    acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
+  }
+  const int k = p.topk;
+  if (k <= 0) return;
+  __syncthreads();
+  MR_STAMP(3);
+
+  // tile top-k: per-thread running lists (songs ascend per thread), per-wave
+  // register tournament, then wave 0 over the NW wave lists.
+  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
+  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
+  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
+  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
+  {
+    long long tk[kMaxTopkLarge];
+    int ts[kMaxTopkLarge];
+#pragma unroll
+    for (int t = 0; t < kMaxTopkLarge; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
+    long long thr = kKeyNone;
+    for (int i = tid; i < bw; i += NT) {
+      const long long key = (long long)acc[i];
+      if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
+    }
+    wave_topk_regs<kMaxTopkLarge>(tk, ts, k, wk + w * k, ws + w * k);
+  }
+  __syncthreads();
+  if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
+  __syncthreads();
+  MR_STAMP(4);
+  if (p.n_tiles == 1) {
+    for (int r = tid; r < k; r += NT) {
+      const size_t o = (size_t)u * k + r;
+      p.top_key[o] = fk[r];
+      p.top_song[o] = fs[r];
+      p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+    }
+  } else {
+    const size_t o = ((size_t)bu * p.n_tiles + tile) * k;  // batch-local user
+    for (int r = tid; r < k; r += NT) {
+      p.cand_key[o + r] = fk[r];
+      p.cand_song[o + r] = fs[r];
+    }
+  }
+  MR_STAMP(5);
+  (void)lane;
+}
+
+// ---------------------------------------------------------------------------
 // pull shape (dense neighbourhoods, e.g. 10k x 1k): stage 1 scatters the
 // neighbour weights of a batch of test users into Yt[v][user] (int64 global
 // atomics: exact and order-independent); a pull kernel then gives each wave
@@ -954,13 +1238,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 // atomics, no tiles of accumulators). Scores go through a per-wave LDS tile
 // for row-contiguous stores; each lane keeps a running top-k of its user.
 // ---------------------------------------------------------------------------
-// Wave-private LDS hand-off: wait for this wave's LDS ops, keep the compiler
-// from reordering across it (a single wave needs no s_barrier).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Bounds-checked diagnostic build (-DMR_CHECKS, libmr_engine_checks.so): an
 // out-of-range index is recorded in *dbg (bit = code) and replaced by 0.
@@ -1247,7 +1524,7 @@ using ColKernel = void (*)(ColParams);
 using PullKernel = void (*)(PullParams);
 
 // Launch shapes (mr_options.stage1 / mr_launch_info).
-enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2 };
+enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2, kShapeWide = 3 };
 
 }  // namespace
 
@@ -1265,7 +1542,7 @@ struct mr_ctx {
   int block_songs = 0, n_tiles = 0;
   int cap = 0, batch = 0;
   int chunk = 1, n_chunks = 1;  // separate shape: stage-1 chunks of train users
-  size_t score_lds = 0, nbr_lds = 0, merge_lds = 0;
+  size_t score_lds = 0, nbr_lds = 0, merge_lds = 0, wide_lds = 0;
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
   NbrKernel nbr_kernel[2] = {nullptr, nullptr};
   ColKernel col_kernel[2] = {nullptr, nullptr};
@@ -1273,7 +1550,8 @@ struct mr_ctx {
   DevBuf<unsigned long long> yt;
   DevBuf<unsigned> dbg;  // MR_CHECKS builds: out-of-range index bits
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
-  DevBuf<int> tr_songs, te_songs, trs_users, blk_ptr, nbr_v, nbr_cnt, cand_song, top_song;
+  DevBuf<int> te_songs, trs_users, toff, nbr_v, nbr_cnt, cand_song, top_song;
+  DevBuf<unsigned short> tsongs;
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
   DevBuf<unsigned char> dense;
@@ -1296,7 +1574,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tr_songs.release(); te_songs.release(); trs_users.release(); blk_ptr.release();
+    tsongs.release(); te_songs.release(); trs_users.release(); toff.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -1350,6 +1628,8 @@ void pick_kernels(mr_ctx* c) {
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, true> : k_score<MODEL, float, true>;
   else
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
+  if (c->shape == kShapeWide)
+    c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads> : k_score_wide<MODEL, float, kWideThreads>;
   c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
   c->col_kernel[MODEL] = k_stage1_columns<MODEL>;
   c->pull_kernel[MODEL] = f64 ? k_pull<MODEL, double> : k_pull<MODEL, float>;
@@ -1397,7 +1677,7 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.out_dtype != MR_OUT_F32 && o.out_dtype != MR_OUT_F64) return fail(MR_E_INVALID, "bad out_dtype %d", o.out_dtype);
   if (o.block_songs < 0 || o.block_songs > kMaxBlockSongs || (o.block_songs % 256) != 0)
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
-  if (o.stage1 < 0 || o.stage1 > 3) return fail(MR_E_INVALID, "stage1 %d outside [0,3]", o.stage1);
+  if (o.stage1 < 0 || o.stage1 > 4) return fail(MR_E_INVALID, "stage1 %d outside [0,4]", o.stage1);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
@@ -1503,9 +1783,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (c->opt.stage1 == 1) shape = kShapeFused;
   else if (c->opt.stage1 == 2) shape = kShapeSeparate;
   else if (c->opt.stage1 == 3) shape = kShapePull;
+  else if (c->opt.stage1 == 4) shape = kShapeWide;
   else if (n_te >= kPullMinUsers && k <= kPullMaxK && n_tr <= kMaxLdsTrainUsers) shape = kShapePull;
+  else if (n_tr > kMaxLdsTrainUsers && k <= kMaxTopkLarge) shape = kShapeWide;
   else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
-  const bool fused = shape == kShapeFused, pull = shape == kShapePull;
+  const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide;
+  if (wide && k > kMaxTopkLarge)
+    return fail(MR_E_INVALID, "wide shape keeps topk <= %d (got %d)", kMaxTopkLarge, k);
   if (fused && n_tr > kMaxFusedTrainUsers)
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
   if (pull && k > kPullMaxK) return fail(MR_E_INVALID, "pull shape keeps topk <= %d (got %d)", kPullMaxK, k);
@@ -1527,7 +1811,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (pull) {
     bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
   } else {
-    bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k, n_tr);
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs
+         : wide               ? (int)std::min<long long>(kMaxBlockSongs, ((long long)width + 255) / 256 * 256)
+                              : auto_block_songs(width, n_te, fused, k, n_tr);
     if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
     if (k > kMaxTopkLarge && bs > kMaxTopkTile)
       return fail(MR_E_INVALID, "with topk > %d block_songs must be <= %d (got %d)", kMaxTopkLarge, kMaxTopkTile, bs);
@@ -1545,30 +1831,40 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   }
   for (int v = 0; v < n_tr; ++v) sqrt_tr[v] = std::sqrt((double)d->tr_len[v]);
   for (int u = 0; u < n_te; ++u) sqrt_te[u] = std::sqrt((double)d->te_len[u]);
-  // Song-tiled row pointers of the train u->s CSR: blk_ptr[v][j] = first
-  // entry of S(v) with song >= min(hi, lo + j*bs).
-  std::vector<int32_t> blk_ptr(pull ? 1 : (size_t)std::max(1, n_tr) * (n_tiles + 1));
-  for (int v = 0; v < (pull ? 0 : n_tr); ++v) {  // one merge walk over the sorted row
-    int64_t i = d->tr_off[v];
-    const int64_t e = d->tr_off[v + 1];
-    int32_t* row = blk_ptr.data() + (size_t)v * (n_tiles + 1);
-    for (int j = 0; j <= n_tiles; ++j) {
-      const int bound = std::min(hi, lo + j * bs);
-      while (i < e && d->tr_songs[i] < bound) ++i;
-      row[j] = (int32_t)i;
+  // Tile-major train CSR over the shard's songs: for tile t, user v, the
+  // tile-local ids of S(v) ∩ [lo + t*bs, lo + (t+1)*bs) live at
+  // tsongs[toff[t*n_tr + v] .. toff[t*n_tr + v + 1]) (entries ordered by
+  // (tile, user, song)), so neighbouring users' segments share cache lines.
+  const size_t n_tv = pull ? 0 : (size_t)n_tiles * n_tr;
+  std::vector<int32_t> toff(n_tv + 1, 0);
+  for (int v = 0; v < (pull ? 0 : n_tr); ++v)
+    for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) {
+      const int s = d->tr_songs[i];
+      if (s >= lo && s < hi) toff[(size_t)((s - lo) / bs) * n_tr + v + 1]++;
     }
+  for (size_t i = 0; i < n_tv; ++i) toff[i + 1] += toff[i];
+  std::vector<uint16_t> tsongs(std::max<int64_t>(1, toff[n_tv]));
+  {
+    std::vector<int32_t> fill(toff.begin(), toff.end() - 1);
+    for (int v = 0; v < (pull ? 0 : n_tr); ++v)
+      for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) {
+        const int s = d->tr_songs[i];
+        if (s < lo || s >= hi) continue;
+        const int t = (s - lo) / bs;
+        tsongs[fill[(size_t)t * n_tr + v]++] = (uint16_t)(s - lo - t * bs);
+      }
   }
   // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = n_chunks * chunk;
   const size_t budget = (size_t)8 << 30;
   const int batch = fused  ? n_te
                     : pull ? std::min(n_te, pull_batch)
-                           : (int)std::max<size_t>(1, std::min<size_t>(n_te, budget / ((size_t)cap * 12)));
+                           : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
+                                                                      budget / ((size_t)cap * 12)));
   const int te_stride = (batch + kPullLanes - 1) / kPullLanes * kPullLanes;
 
   hipStream_t st = c->stream;
   if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(d->tr_off), (size_t)n_tr + 1, st))) return rc;
-  if ((rc = dev_upload(c->tr_songs, d->tr_songs, (size_t)d->tr_off[n_tr], st))) return rc;
   if ((rc = dev_upload(c->te_off, reinterpret_cast<const long long*>(d->te_off), (size_t)n_te + 1, st))) return rc;
   if ((rc = dev_upload(c->te_songs, d->te_songs, (size_t)d->te_off[n_te], st))) return rc;
   if ((rc = dev_upload(c->trs_off, reinterpret_cast<const long long*>(trs_off.data()), trs_off.size(), st))) return rc;
@@ -1577,7 +1873,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->sqrt_c, sqrt_c.data(), sqrt_c.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
-  if ((rc = dev_upload(c->blk_ptr, blk_ptr.data(), blk_ptr.size(), st))) return rc;
+  if ((rc = dev_upload(c->toff, toff.data(), toff.size(), st))) return rc;
+  if ((rc = dev_upload(c->tsongs, tsongs.data(), tsongs.size(), st))) return rc;
   if (pull) {
     if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
     if ((rc = dev_alloc(c->dbg, 1))) return rc;
@@ -1588,7 +1885,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
   }
   if (k > 0) {
-    const size_t nc = (size_t)(pull ? te_stride : n_te) * n_tiles * k;
+    const size_t nc = (size_t)(pull ? te_stride : wide ? batch : n_te) * n_tiles * k;
     if ((rc = dev_alloc(c->cand_key, nc))) return rc;
     if ((rc = dev_alloc(c->cand_song, nc))) return rc;
     if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
@@ -1602,10 +1899,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
 
   c->fused = fused;
   c->shape = shape;
+  c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
   c->te_stride = te_stride;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
-  c->score_lds = pull ? 0 : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
+  c->score_lds = pull ? 0 : wide ? c->wide_lds
+                                  : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
                 c->score_lds);
@@ -1618,7 +1917,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     MR_HIP(hipFuncSetAttribute((const void*)c->col_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
   }
-  if (pull && k > 0) {
+  if ((pull || wide) && k > 0) {
     c->merge_lds = (size_t)merge_lds_bytes(k);
     MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->merge_lds));
@@ -1691,7 +1990,7 @@ int run_model(mr_ctx* c, int model) {
       c->ring_used++;
       MR_HIP(hipEventRecord(ev[0], st));
     }
-    if (c->shape == kShapeSeparate) {
+    if (c->shape == kShapeSeparate || c->shape == kShapeWide) {
       if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) return fail(MR_E_STATE, "separate shape without neighbour buffers");
       NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->chunk, c->n_chunks, c->te_off.p, c->te_songs.p,
                    c->trs_off.p, c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
@@ -1757,7 +2056,8 @@ int run_model(mr_ctx* c, int model) {
     for (int y0 = 0; y0 < nb; y0 += 65528) {
       const int ny = std::min(65528, nb - y0);
       // separate shape: all tiles of a user on one XCD (grid padded to 8 users)
-      const int remap = c->shape == kShapeSeparate && c->n_tiles > 1;
+      const bool wide = c->shape == kShapeWide;
+      const int remap = (c->shape == kShapeSeparate && c->n_tiles > 1) || wide;
       const int gy = remap ? (ny + 7) / 8 * 8 : ny;
       ScoreParams sp{};
       sp.chunk = c->chunk; sp.n_chunks = c->n_chunks;
@@ -1768,7 +2068,7 @@ int run_model(mr_ctx* c, int model) {
       sp.block_songs = c->block_songs; sp.n_tiles = c->n_tiles;
       sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
-      sp.tr_songs = c->tr_songs.p; sp.blk_ptr = c->blk_ptr.p; sp.sqrt_c = c->sqrt_c.p;
+      sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.sqrt_c = c->sqrt_c.p;
       sp.trs_off = c->trs_off.p; sp.trs_users = c->trs_users.p; sp.q_song = c->q_song.p;
       sp.sqrt_tr = c->sqrt_tr.p; sp.sqrt_te = c->sqrt_te.p;
       sp.cap = c->cap;
@@ -1779,8 +2079,16 @@ int run_model(mr_ctx* c, int model) {
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
-      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(kThreads), c->score_lds, st, sp);
+      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
+                         c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
+      if (wide && k > 0 && c->n_tiles > 1) {  // per-user top-k over the tiles' candidates
+        MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,
+                       c->top_key.p + (size_t)(user0 + y0) * k, c->top_song.p + (size_t)(user0 + y0) * k,
+                       c->top_score.p + (size_t)(user0 + y0) * k, c->dbg.p, 0, 0};
+        hipLaunchKernelGGL(k_topk_merge, dim3(ny), dim3(kThreads), c->merge_lds, st, mp);
+        MR_HIP(hipGetLastError());
+      }
       if (c->win_open) c->win_launches++;
     }
     if (timed) MR_HIP(hipEventRecord(ev[2], st));

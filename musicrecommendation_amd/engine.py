@@ -42,7 +42,7 @@ class Engine:
         opt.topk = topk
         opt.dense = 1 if dense else 0
         opt.time_kernels = 1 if time_kernels else 0
-        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3}[stage1]
+        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4}[stage1]
         opt.stage1_chunk = stage1_chunk
         self.opt = opt
         self.dtype = np.float32 if out_dtype == "f32" else np.float64
@@ -64,7 +64,7 @@ class Engine:
         fz, bsz, nt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self._L.mr_launch_info(self._h, ctypes.byref(fz), ctypes.byref(bsz), ctypes.byref(nt)),
                    "mr_launch_info")
-        self.shape = {0: "separate", 1: "fused", 2: "pull"}[fz.value]
+        self.shape = {0: "separate", 1: "fused", 2: "pull", 3: "wide"}[fz.value]
         self.fused, self.block_songs, self.n_tiles = self.shape == "fused", bsz.value, nt.value
 
     # ---- lifecycle ----------------------------------------------------------

@@ -130,9 +130,21 @@ def calibrate_alpha(n_train: int, n_test: int, seed: int, target_songs: int,
     return round(best[1], 6)
 
 
+# Full-scale configs (bulk generator, capped Zipf head; SURVEY.md §8d seeds):
+# C4 = the full Taste Profile (1,019,318 users) with the last 10,000 as test
+# users; C5 = 2,000 test users against the remaining train set.
+BULK_CONFIGS = {
+    "c4": (1_009_318, 10_000, 4),
+    "c5": (1_017_318, 2_000, 5),
+}
+
+
 def config(name: str, n_test: Optional[int] = None) -> Triplets:
     """Named config; n_test overrides the test-user count (weak-scaling runs
     use n_test = 10 x GPUs with the same train set and the same alpha)."""
+    if name in BULK_CONFIGS:
+        n_tr, n_te, seed = BULK_CONFIGS[name]
+        return generate_bulk(n_tr, n_test if n_test is not None else n_te, seed)
     n_tr, n_te, seed, target = CONFIGS[name]
     alpha = ALPHA.get(name)
     if alpha is None and target is not None:

@@ -112,13 +112,26 @@ def test_wide_tiles_c2(block, model, k):
         check_exact(ds, model, k=k, stage1="fused", block_songs=block)
 
 
+@pytest.mark.parametrize("k", [1, 10, 16])
+@pytest.mark.parametrize("chunk", [0, 7])
+@pytest.mark.parametrize("model", MODELS)
+def test_wide_shape_small_inputs(model, chunk, k):
+    """The wide kernel (1024-thread workgroups, separate merge launch) on the
+    fixtures and C2: one tile and many tiles, chunked and unchunked stage 1."""
+    for ds in (synth_fixture("small")[0], synth.config("c2", n_test=13).dataset()):
+        for block in (256, 2048, 16384):
+            check_exact(ds, model, k=k, stage1="wide", stage1_chunk=chunk, block_songs=block)
+    with pytest.raises(_lib.EngineError):
+        Engine(synth_fixture("tiny")[0], stage1="wide", topk=17)
+
+
 @pytest.mark.parametrize("model", MODELS)
 def test_large_train_set_exact(model):
     """n_train > 16384: chunked stage 1 (8192 train users per LDS chunk),
     16384-song tiles, XCD-grouped tiles; every user exact vs the oracle."""
     ds = synth.generate_bulk(40_000, 21, 4).dataset()
     with Engine(ds, out_dtype="f64", topk=10) as e:
-        assert e.shape == "separate" and e.block_songs == 16384
+        assert e.shape == "wide" and e.block_songs == 16384
         e.run(model)
         dense = e.dense()
         songs, _, keys = e.topk()
