@@ -1080,6 +1080,12 @@ __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
 }
 
 constexpr int kWideThreads = 1024;
+#ifndef MR_WIDE_R
+#define MR_WIDE_R 4         // neighbours per thread per iteration (wide kernel; 2/4/8 within 3%)
+#endif
+#ifndef MR_WIDE_PREFETCH
+#define MR_WIDE_PREFETCH 0  // 1 = load the next iteration's list entries ahead
+#endif
 
 template <int MODEL, typename OutT, int NT>
 __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
@@ -1132,11 +1138,9 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
     const int* toff_t = p.toff + (size_t)tile * p.n_tr;
-    constexpr int R = 2, kSeg = 4;
+    constexpr int R = MR_WIDE_R, kSeg = 4;
     int cur = 0;
-    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
-      int v[R], a[R], b[R];
-      unsigned long long q[R];
+    auto load_list = [&](int k0, int (&v)[R], unsigned long long (&q)[R]) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int k = k0 + r * NT;
@@ -1149,6 +1153,22 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           q[r] = (unsigned long long)nq[idx];
         }
       }
+    };
+#if MR_WIDE_PREFETCH
+    int vn[R];
+    unsigned long long qn[R];
+    load_list(tid, vn, qn);
+#endif
+    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
+      int v[R], a[R], b[R];
+      unsigned long long q[R];
+#if MR_WIDE_PREFETCH
+#pragma unroll
+      for (int r = 0; r < R; ++r) { v[r] = vn[r]; q[r] = qn[r]; }
+      load_list(k0 + R * NT, vn, qn);  // next iteration's entries, in flight during this one
+#else
+      load_list(k0, v, q);
+#endif
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         a[r] = b[r] = 0;
