@@ -158,6 +158,31 @@ int mr_sync(mr_ctx* ctx);
 int mr_device_outputs(const mr_ctx* ctx, void** dense, int32_t** topk_songs,
                       int64_t** topk_keys, double** topk_scores);
 
+/* mr_run with the dense model written to a caller-owned DEVICE buffer of
+ * n_te * (song_hi - song_lo) elements of the context's out_dtype (instead of
+ * the context's own buffer); top-k as mr_run. Asynchronous on the context
+ * stream. Lets a caller keep several models on the device (e.g. ubm and ibm
+ * for the combination models below). */
+int mr_run_into(mr_ctx* ctx, int model, void* dense_dev);
+
+/* Device-side view of a loaded context, for companion calls and callers that
+ * launch their own work on the same data (pointers valid until mr_load /
+ * mr_destroy). */
+typedef struct mr_view {
+  int32_t n_test_users, n_songs, song_lo, song_hi, out_dtype, device;
+  const int64_t* te_off;   /* device [n_test_users + 1] */
+  const int32_t* te_songs; /* device, sorted per user (T(u)) */
+  void* stream;            /* hipStream_t of the context */
+} mr_view;
+int mr_view_get(const mr_ctx* ctx, mr_view* view);
+
+/* Top-k of a dense model on the device (e.g. a combination model): per test
+ * user, the k unheard songs of the shard with the highest score, ordered by
+ * (score desc, song id asc), into the context's top-k outputs (read them with
+ * mr_copy_topk / mr_device_outputs). k must equal the context's topk and be
+ * <= 16; scores must be >= 0 (else MR_E_INVALID). Synchronous. */
+int mr_topk_dense_device(mr_ctx* ctx, const void* dense_dev, int32_t k);
+
 /* Synchronous convenience calls: run + copy to caller-allocated host buffers.
  * out: n_te * (song_hi - song_lo) elements of the context's out_dtype. */
 int mr_score_dense(mr_ctx* ctx, int model, void* out);
@@ -183,6 +208,35 @@ int mr_topk_merge_host(int32_t n_shards, int32_t n_te, int32_t k,
 int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
                          const int32_t* songs_in, const int64_t* keys_in, const double* scores_in,
                          int32_t* songs_out, int64_t* keys_out, double* scores_out);
+
+/* ---- combination models and evaluation on the device (MR:317-481, MR:521-639) ----
+ * Over dense models of the context's shard (device pointers, n_te x width of
+ * the context's out_dtype, NaN = no pair), e.g. filled by mr_run_into. Pairs
+ * are indexed in the driver's sorted order (main.scala:57-59: user, then song,
+ * heard songs skipped); pair_base = index of this context's first pair in the
+ * full model (0 unless the context holds a block of test users), n_pairs = the
+ * full model's length. All three are synchronous. */
+#define MR_COMB_LINEAR      0 /* getLinearCombinationModel MR:317-351: ubm*param + ibm*(1-param) */
+#define MR_COMB_AGGREGATION 1 /* getAggregationModel MR:361-418: pairs < (int)(param*n_pairs) from ibm */
+#define MR_COMB_STOCHASTIC  2 /* getStochasticCombinationModel MR:429-481: ibm where u(seed,pair) < param;
+                                 u = 24-bit uniform of splitmix64(seed + (idx+1)*0x9E3779B97F4A7C15) */
+int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_t pair_base, int64_t n_pairs,
+                      const void* ubm, const void* ibm, void* out);
+/* evaluateModel (MR:636), device part: min / max over the model's scores
+ * (MR:524-525; +inf / -inf when the shard holds no pair) ... */
+int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx);
+/* ... and per song s of the shard and threshold t_i = i/10 (MR:590):
+ * pred_counts[s][i] = #test users with (x - mn)/(mx - mn) > t_i (MR:529),
+ * tp_counts[s][i] = those of them whose labels hold s (MR:545). mn/mx are the
+ * GLOBAL extremes (reduce over shards first). Labels: host CSR over the
+ * context's test users, global song ids (label-only songs >= n_songs). */
+int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts);
+/* Host part: AP per song class (MR:588-618, left folds as List.sum) and mAP =
+ * sum / n_label_songs (MR:625-627), classes summed in song-id order. pos[s] =
+ * #test users whose labels hold s. */
+int mr_eval_map(int32_t n_classes, const int32_t* pred_counts, const int32_t* tp_counts, const int32_t* pos,
+                int32_t n_label_songs, double* map_out);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
  * (0 = separate stage-1 kernel — neighbour lists or pull columns —, 1 = the

@@ -75,6 +75,25 @@ class MrOptions(ctypes.Structure):
     ]
 
 
+class MrView(ctypes.Structure):
+    _fields_ = [
+        ("n_test_users", c_int32),
+        ("n_songs", c_int32),
+        ("song_lo", c_int32),
+        ("song_hi", c_int32),
+        ("out_dtype", c_int32),
+        ("device", c_int32),
+        ("te_off", c_void_p),
+        ("te_songs", c_void_p),
+        ("stream", c_void_p),
+    ]
+
+
+MR_COMB_LINEAR = 0
+MR_COMB_AGGREGATION = 1
+MR_COMB_STOCHASTIC = 2
+
+
 class EngineError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str):
         super().__init__(f"{where}: {_ERRNAMES.get(code, code)}: {msg}")
@@ -105,6 +124,13 @@ SIGNATURES = {
     "mr_timing_begin": (c_int, [c_void_p]),
     "mr_timing_end": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double)]),
     "mr_stream": (c_void_p, [c_void_p]),
+    "mr_run_into": (c_int, [c_void_p, c_int, c_void_p]),
+    "mr_view_get": (c_int, [c_void_p, POINTER(MrView)]),
+    "mr_topk_dense_device": (c_int, [c_void_p, c_void_p, c_int32]),
+    "mr_combine_device": (c_int, [c_void_p, c_int, c_double, ctypes.c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mr_eval_minmax_device": (c_int, [c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)]),
+    "mr_eval_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mr_eval_map": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double)]),
     "mr_last_error": (c_char_p, []),
     "mr_corpus_from_tsv": (c_int, [c_char_p, c_char_p, c_char_p, POINTER(c_void_p)]),
     "mr_corpus_dataset": (c_int, [c_void_p, POINTER(MrDataset)]),

@@ -1250,6 +1250,58 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// top-k over a dense model buffer (any model of the context's shape, e.g. a
+// combination model, MR:317-481): one 1024-thread workgroup per test user,
+// per-thread running lists, per-wave register tournament, wave 0 merges.
+// Keys are the bit patterns of the (non-negative) scores; a negative score
+// sets *neg (the caller reports MR_E_INVALID: no total order in int64 keys).
+// ---------------------------------------------------------------------------
+struct DenseTopkParams {
+  int user0, width, song_lo, k;
+  const void* dense;
+  long long* top_key;
+  int* top_song;
+  double* top_score;
+  unsigned* neg;
+};
+
+template <typename OutT>
+__global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) {
+  constexpr int NT = kWideThreads, NW = NT / 64;
+  __shared__ long long wk[NW * kMaxTopkLarge];
+  __shared__ int ws[NW * kMaxTopkLarge];
+  __shared__ long long fk[kMaxTopkLarge];
+  __shared__ int fs[kMaxTopkLarge];
+  const int u = p.user0 + blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, k = p.k;
+  const OutT* row = reinterpret_cast<const OutT*>(p.dense) + (size_t)u * p.width;
+  long long tk[kMaxTopkLarge];
+  int ts[kMaxTopkLarge];
+#pragma unroll
+  for (int t = 0; t < kMaxTopkLarge; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
+  long long thr = kKeyNone;
+  bool neg = false;
+  for (int i = tid; i < p.width; i += NT) {
+    const double x = (double)row[i];
+    if (x != x) continue;  // NaN: no pair (heard song, MR:109)
+    if (x < 0.0) { neg = true; continue; }
+    const long long key = __double_as_longlong(x + 0.0);  // -0.0 -> +0.0
+    if (key > thr) lane_list_insert(tk, ts, k, key, p.song_lo + i, thr);
+  }
+  if (neg) atomicOr(p.neg, 1u);
+  wave_topk_regs<kMaxTopkLarge>(tk, ts, k, wk + w * k, ws + w * k);
+  __syncthreads();
+  if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
+  __syncthreads();
+  for (int r = tid; r < k; r += NT) {
+    const size_t o = (size_t)u * k + r;
+    p.top_key[o] = fk[r];
+    p.top_song[o] = fs[r];
+    p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // pull shape (dense neighbourhoods, e.g. 10k x 1k): stage 1 scatters the
 // neighbour weights of a batch of test users into Yt[v][user] (int64 global
 // atomics: exact and order-independent); a pull kernel then gives each wave
@@ -1589,6 +1641,8 @@ struct mr_ctx {
   // number of mr_run calls, no per-launch events.
   hipEvent_t win[2] = {nullptr, nullptr};
   bool win_open = false;
+  void* dense_override = nullptr;  // mr_run_into: caller's device buffer for this run's dense model
+  DevBuf<unsigned> flag;           // mr_topk_dense_device: negative-score flag
   long long win_launches = 0;
 
   void release_data() {
@@ -1602,6 +1656,7 @@ struct mr_ctx {
     stamps.release();
     yt.release();
     dbg.release();
+    flag.release();
     loaded = ran = false;
   }
 };
@@ -1916,6 +1971,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   }
   const size_t esz = c->opt.out_dtype == MR_OUT_F64 ? 8 : 4;
   if ((rc = dev_alloc(c->dense, c->opt.dense ? (size_t)n_te * width * esz : 1))) return rc;
+  if ((rc = dev_alloc(c->flag, 1))) return rc;
 
   c->fused = fused;
   c->shape = shape;
@@ -2045,7 +2101,7 @@ int run_model(mr_ctx* c, int model) {
       pp.frac_bits = c->opt.frac_bits; pp.topk = k; pp.dense = c->opt.dense;
       pp.Yt = c->yt.p; pp.trs_off = c->trs_off.p; pp.trs_users = c->trs_users.p; pp.sqrt_c = c->sqrt_c.p;
       pp.te_off = c->te_off.p; pp.te_songs = c->te_songs.p;
-      pp.dense_out = c->dense.p; pp.cand_key = c->cand_key.p; pp.cand_song = c->cand_song.p;
+      pp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p; pp.cand_key = c->cand_key.p; pp.cand_song = c->cand_song.p;
       pp.dbg = c->dbg.p;
       pp.n_yt = (long long)c->yt.n; pp.n_trs = (long long)c->trs_users.n; pp.n_te_songs = (long long)c->te_songs.n;
       pp.n_te_off = (long long)c->te_off.n; pp.n_songs1 = (long long)c->trs_off.n;
@@ -2095,7 +2151,7 @@ int run_model(mr_ctx* c, int model) {
       sp.nbr_v = c->fused ? nullptr : c->nbr_v.p + (size_t)y0 * c->cap;
       sp.nbr_q = c->fused ? nullptr : c->nbr_q.p + (size_t)y0 * c->cap;
       sp.nbr_cnt = c->fused ? nullptr : c->nbr_cnt.p + (size_t)y0 * c->n_chunks;
-      sp.dense_out = c->dense.p;
+      sp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p;
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
@@ -2271,6 +2327,57 @@ int mr_kernel_times(mr_ctx* c, int32_t which, int64_t* launches, double* total_m
   if (launches) *launches = c->launches[which];
   if (total_ms) *total_ms = c->ms[which];
   if (reset) { c->launches[which] = 0; c->ms[which] = 0.0; }
+  return MR_OK;
+}
+
+int mr_run_into(mr_ctx* c, int model, void* dense_dev) {
+  if (!c || !dense_dev) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_run_into before mr_load");
+  if (!c->opt.dense) return fail(MR_E_STATE, "context created with dense=0");
+  c->dense_override = dense_dev;
+  const int rc = mr_run(c, model);
+  c->dense_override = nullptr;
+  return rc;
+}
+
+int mr_view_get(const mr_ctx* c, mr_view* v) {
+  if (!c || !v) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_view_get before mr_load");
+  std::memset(v, 0, sizeof *v);
+  v->n_test_users = c->n_te;
+  v->n_songs = c->n_s;
+  v->song_lo = c->song_lo;
+  v->song_hi = c->song_hi;
+  v->out_dtype = c->opt.out_dtype;
+  v->device = c->opt.device;
+  v->te_off = reinterpret_cast<const int64_t*>(c->te_off.p);
+  v->te_songs = c->te_songs.p;
+  v->stream = (void*)c->stream;
+  return MR_OK;
+}
+
+int mr_topk_dense_device(mr_ctx* c, const void* dense_dev, int32_t k) {
+  if (!c || !dense_dev) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_topk_dense_device before mr_load");
+  if (k != c->opt.topk || k <= 0 || k > kMaxTopkLarge)
+    return fail(MR_E_INVALID, "k=%d must equal the context's topk (%d) and be in [1,%d]", k, c->opt.topk,
+                kMaxTopkLarge);
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipMemsetAsync(c->flag.p, 0, sizeof(unsigned), c->stream));
+  const bool f64 = c->opt.out_dtype == MR_OUT_F64;
+  for (int y0 = 0; y0 < c->n_te; y0 += 65535) {
+    DenseTopkParams tp{y0, c->width, c->song_lo, k, dense_dev, c->top_key.p, c->top_song.p, c->top_score.p,
+                       c->flag.p};
+    const int ny = std::min(65535, c->n_te - y0);
+    if (f64) hipLaunchKernelGGL(k_topk_dense<double>, dim3(ny), dim3(kWideThreads), 0, c->stream, tp);
+    else hipLaunchKernelGGL(k_topk_dense<float>, dim3(ny), dim3(kWideThreads), 0, c->stream, tp);
+    MR_HIP(hipGetLastError());
+  }
+  unsigned neg = 0;
+  MR_HIP(hipMemcpyAsync(&neg, c->flag.p, sizeof neg, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  if (neg) return fail(MR_E_INVALID, "dense model has negative scores: top-k keys need scores >= 0");
+  c->ran = true;
   return MR_OK;
 }
 

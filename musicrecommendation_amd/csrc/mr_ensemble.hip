@@ -1,0 +1,307 @@
+// mr_ensemble.hip — combination models and the reference's threshold mAP on
+// the device, over dense models of one context's shard (n_te x width of the
+// context's out_dtype, NaN = no pair). MR = MusicRecommender.scala:
+//   getLinearCombinationModel(P)      MR:317-351  out = ubm*alpha + ibm*(1-alpha)
+//   getAggregationModel(P)            MR:361-418  pair index < (int)(p*P) -> ibm, else ubm
+//   getStochasticCombinationModel(P)  MR:429-481  nextFloat() < p -> ibm, else ubm; the
+//                                     reference's java.util.Random is unseeded, here a
+//                                     seeded counter-based stream over the pair index
+//   evaluateModel                     MR:521-639  global min/max (MR:524-525), per-class
+//                                     confusion counts at the 10 thresholds (MR:541-553,
+//                                     MR:590); AP and the mean on the host (mr_eval_map)
+// The pair index is the position of (u, s) in the driver's sorted model
+// (main.scala:57-59 sorts by (user, song): the interned order, heard songs
+// skipped): idx(u, s) = pair_base + u*n_s - te_off[u] + s - |{t in T(u): t < s}|.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "mr_engine.h"
+
+namespace mr_host {
+int fail(int code, const char* fmt, ...);  // thread-local error slot (mr_engine.hip)
+}
+
+namespace {
+
+using mr_host::fail;
+
+#define MR_HIP(call)                                                                            \
+  do {                                                                                          \
+    hipError_t e_ = (call);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail(e_ == hipErrorOutOfMemory ? MR_E_OOM : MR_E_HIP, "%s failed: %s (%s:%d)", #call, \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                                   \
+  } while (0)
+
+constexpr int kThreads = 256;
+constexpr int kThresholds = 10;  // 0.0, 0.1, ..., 0.9 (MR:590)
+__constant__ double kThr[kThresholds] = {0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9};
+
+// ---- combination models -----------------------------------------------------
+struct CombParams {
+  int n_te, width, song_lo, n_songs, kind;
+  double param;
+  unsigned long long seed;
+  long long pair_base, threshold;
+  const long long* te_off;
+  const int* te_songs;
+  const void* ubm;
+  const void* ibm;
+  void* out;
+};
+
+// splitmix64 finaliser over (seed, pair index): a stateless stream, so every
+// pair's draw is independent of launch geometry and shard count.
+__host__ __device__ inline unsigned long long splitmix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// 24 random bits / 2^24, the distribution of java.util.Random.nextFloat.
+__host__ __device__ inline float pair_uniform(unsigned long long seed, long long idx) {
+  const unsigned long long z = splitmix64(seed + (unsigned long long)(idx + 1) * 0x9E3779B97F4A7C15ull);
+  return (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void k_combine(CombParams p) {
+  const int u = blockIdx.y;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= p.width) return;
+  const size_t o = (size_t)u * p.width + i;
+  const OutT* ubm = reinterpret_cast<const OutT*>(p.ubm);
+  const OutT* ibm = reinterpret_cast<const OutT*>(p.ibm);
+  OutT* out = reinterpret_cast<OutT*>(p.out);
+  if (p.kind == MR_COMB_LINEAR) {  // MR:327: rank1 * alpha + rank2 * (1 - alpha); NaN stays NaN
+    out[o] = (OutT)((double)ubm[o] * p.param + (double)ibm[o] * (1.0 - p.param));
+    return;
+  }
+  const int s = p.song_lo + i;
+  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  long long a = t0, b = t1;  // first song of T(u) >= s
+  while (a < b) {
+    const long long m = (a + b) >> 1;
+    if (p.te_songs[m] < s) a = m + 1; else b = m;
+  }
+  if (a < t1 && p.te_songs[a] == s) {  // heard: no pair (MR:109)
+    out[o] = (OutT)NAN;
+    return;
+  }
+  const long long idx = p.pair_base + (long long)u * p.n_songs - t0 + s - (a - t0);
+  const bool take_ibm = p.kind == MR_COMB_AGGREGATION ? idx < p.threshold                   // MR:380-381
+                                                      : (double)pair_uniform(p.seed, idx) < p.param;  // MR:414-415
+  out[o] = take_ibm ? ibm[o] : ubm[o];
+}
+
+// ---- evaluation ------------------------------------------------------------
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void k_minmax(const OutT* d, long long n, double* part) {
+  __shared__ double smn[kThreads], smx[kThreads];
+  double mn = INFINITY, mx = -INFINITY;
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const double x = (double)d[i];
+    if (x != x) continue;
+    mn = fmin(mn, x);
+    mx = fmax(mx, x);
+  }
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (int h = kThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + h]);
+      smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + h]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = smn[0];
+    part[2 * blockIdx.x + 1] = smx[0];
+  }
+}
+
+struct EvalParams {
+  int n_te, width, song_lo, users_per_block;
+  double mn, mx;
+  const void* dense;
+  int* pred;  // [width][10]: users with (x - min) / (max - min) > t_i (MR:529)
+  int* tp;    // [width][10]: of those, users whose labels hold the song (MR:545)
+  const int* lab_u;
+  const int* lab_s;
+  long long n_lab;
+};
+
+__device__ __forceinline__ int levels(double x, double mn, double mx) {
+  const double v = (x - mn) / (mx - mn);  // MR:529 (NaN > t is false)
+  int c = 0;
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t) c += v > kThr[t] ? 1 : 0;
+  return c;  // thresholds ascend: predicted at t_i for every i < c
+}
+
+// one thread per song column, a block of users per blockIdx.y (rows read coalesced)
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= p.width) return;
+  const int u0 = blockIdx.y * p.users_per_block, u1 = min(p.n_te, u0 + p.users_per_block);
+  const OutT* d = reinterpret_cast<const OutT*>(p.dense);
+  int cnt[kThresholds];
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t) cnt[t] = 0;
+  for (int u = u0; u < u1; ++u) {
+    const double x = (double)d[(size_t)u * p.width + i];
+    if (x != x) continue;
+    const int c = levels(x, p.mn, p.mx);
+#pragma unroll
+    for (int t = 0; t < kThresholds; ++t) cnt[t] += t < c ? 1 : 0;
+  }
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t)
+    if (cnt[t]) atomicAdd(&p.pred[(size_t)i * kThresholds + t], cnt[t]);
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void k_eval_tp(EvalParams p) {
+  const long long j = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= p.n_lab) return;
+  const int u = p.lab_u[j], g = p.lab_s[j] - p.song_lo;
+  if (g < 0 || g >= p.width) return;  // other shard, or a label-only song (never predicted)
+  const double x = (double)reinterpret_cast<const OutT*>(p.dense)[(size_t)u * p.width + g];
+  if (x != x) return;
+  const int c = levels(x, p.mn, p.mx);
+  for (int t = 0; t < c; ++t) atomicAdd(&p.tp[(size_t)g * kThresholds + t], 1);
+}
+
+template <typename T>
+struct Tmp {  // scratch device buffer of one call
+  T* p = nullptr;
+  ~Tmp() { if (p) (void)hipFree(p); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_t pair_base, int64_t n_pairs,
+                      const void* ubm, const void* ibm, void* out) {
+  if (!ctx || !ubm || !ibm || !out) return fail(MR_E_INVALID, "null argument");
+  if (kind != MR_COMB_LINEAR && kind != MR_COMB_AGGREGATION && kind != MR_COMB_STOCHASTIC)
+    return fail(MR_E_INVALID, "unknown combination kind %d", kind);
+  // MR:366-369 / MR:434-437: the reference prints and calls System.exit(-1)
+  if (kind != MR_COMB_LINEAR && !(param >= 0.0 && param <= 1.0))
+    return fail(MR_E_INVALID, "percentage/probability %g must be between 0 and 1", param);
+  mr_view v;
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  if (pair_base < 0 || n_pairs < 0) return fail(MR_E_INVALID, "negative pair_base / n_pairs");
+  MR_HIP(hipSetDevice(v.device));
+  const int width = v.song_hi - v.song_lo;
+  CombParams cp{v.n_test_users, width, v.song_lo, v.n_songs, kind, param, (unsigned long long)seed,
+                (long long)pair_base, (long long)(param * (double)n_pairs),  // (p * length).toInt, MR:371
+                reinterpret_cast<const long long*>(v.te_off), v.te_songs, ubm, ibm, out};
+  hipStream_t st = (hipStream_t)v.stream;
+  for (int y0 = 0; y0 < v.n_test_users; y0 += 65535) {
+    CombParams q = cp;
+    const int ny = std::min(65535, v.n_test_users - y0);
+    const size_t esz = v.out_dtype == MR_OUT_F64 ? 8 : 4;
+    q.n_te = ny;
+    q.te_off = cp.te_off + y0;  // values index the whole te_songs: pairs before user y0 + u are
+    q.pair_base = cp.pair_base + (long long)y0 * v.n_songs;  // (y0 + u) * n_s - te_off[y0 + u]
+    q.ubm = (const char*)ubm + (size_t)y0 * width * esz;
+    q.ibm = (const char*)ibm + (size_t)y0 * width * esz;
+    q.out = (char*)out + (size_t)y0 * width * esz;
+    dim3 grid((width + kThreads - 1) / kThreads, ny);
+    if (v.out_dtype == MR_OUT_F64) hipLaunchKernelGGL(k_combine<double>, grid, dim3(kThreads), 0, st, q);
+    else hipLaunchKernelGGL(k_combine<float>, grid, dim3(kThreads), 0, st, q);
+    MR_HIP(hipGetLastError());
+  }
+  MR_HIP(hipStreamSynchronize(st));
+  return MR_OK;
+}
+
+int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx) {
+  if (!ctx || !dense || !mn || !mx) return fail(MR_E_INVALID, "null argument");
+  mr_view v;
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  MR_HIP(hipSetDevice(v.device));
+  const long long n = (long long)v.n_test_users * (v.song_hi - v.song_lo);
+  const int blocks = (int)std::max<long long>(1, std::min<long long>(1024, (n + kThreads - 1) / kThreads));
+  Tmp<double> part;
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&part.p), (size_t)blocks * 2 * sizeof(double)));
+  hipStream_t st = (hipStream_t)v.stream;
+  if (v.out_dtype == MR_OUT_F64)
+    hipLaunchKernelGGL(k_minmax<double>, dim3(blocks), dim3(kThreads), 0, st, (const double*)dense, n, part.p);
+  else
+    hipLaunchKernelGGL(k_minmax<float>, dim3(blocks), dim3(kThreads), 0, st, (const float*)dense, n, part.p);
+  MR_HIP(hipGetLastError());
+  std::vector<double> h((size_t)blocks * 2);
+  MR_HIP(hipMemcpyAsync(h.data(), part.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+  MR_HIP(hipStreamSynchronize(st));
+  double a = INFINITY, b = -INFINITY;
+  for (int i = 0; i < blocks; ++i) {
+    a = std::fmin(a, h[2 * i]);
+    b = std::fmax(b, h[2 * i + 1]);
+  }
+  *mn = a;
+  *mx = b;
+  return MR_OK;
+}
+
+int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts) {
+  if (!ctx || !dense || !lab_off || !pred_counts || !tp_counts) return fail(MR_E_INVALID, "null argument");
+  mr_view v;
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  MR_HIP(hipSetDevice(v.device));
+  const int width = v.song_hi - v.song_lo, n_te = v.n_test_users;
+  const long long n_lab = lab_off[n_te];
+  if (n_lab > 0 && !lab_songs) return fail(MR_E_INVALID, "null label songs");
+  std::vector<int32_t> lu((size_t)std::max<long long>(1, n_lab)), ls((size_t)std::max<long long>(1, n_lab));
+  for (int u = 0; u < n_te; ++u)
+    for (int64_t j = lab_off[u]; j < lab_off[u + 1]; ++j) {
+      if (j < 0 || j >= n_lab || lab_off[u + 1] < lab_off[u]) return fail(MR_E_INVALID, "bad label CSR");
+      lu[j] = u;
+      ls[j] = lab_songs[j];
+    }
+  Tmp<int> d_pred, d_tp, d_lu, d_ls;
+  const size_t nc = (size_t)width * kThresholds;
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_pred.p), std::max<size_t>(1, nc) * 4));
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_tp.p), std::max<size_t>(1, nc) * 4));
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_lu.p), lu.size() * 4));
+  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_ls.p), ls.size() * 4));
+  hipStream_t st = (hipStream_t)v.stream;
+  MR_HIP(hipMemsetAsync(d_pred.p, 0, nc * 4, st));
+  MR_HIP(hipMemsetAsync(d_tp.p, 0, nc * 4, st));
+  MR_HIP(hipMemcpyAsync(d_lu.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, st));
+  MR_HIP(hipMemcpyAsync(d_ls.p, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, st));
+  // enough (song block x user block) workgroups to fill the chip
+  const int sx = (width + kThreads - 1) / kThreads;
+  const int uy = std::max(1, std::min(n_te, (2048 + sx - 1) / sx));
+  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
+                n_lab};
+  const bool f64 = v.out_dtype == MR_OUT_F64;
+  if (width > 0) {
+    if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+    else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+    MR_HIP(hipGetLastError());
+  }
+  if (n_lab > 0) {
+    const int lb = (int)((n_lab + kThreads - 1) / kThreads);
+    if (f64) hipLaunchKernelGGL(k_eval_tp<double>, dim3(lb), dim3(kThreads), 0, st, ep);
+    else hipLaunchKernelGGL(k_eval_tp<float>, dim3(lb), dim3(kThreads), 0, st, ep);
+    MR_HIP(hipGetLastError());
+  }
+  MR_HIP(hipMemcpyAsync(pred_counts, d_pred.p, nc * 4, hipMemcpyDeviceToHost, st));
+  MR_HIP(hipMemcpyAsync(tp_counts, d_tp.p, nc * 4, hipMemcpyDeviceToHost, st));
+  MR_HIP(hipStreamSynchronize(st));
+  return MR_OK;
+}
+
+}  // extern "C"

@@ -250,4 +250,27 @@ int mr_topk_merge_host(int32_t n_shards, int32_t n_te, int32_t k, const int32_t*
   return MR_OK;
 }
 
+int mr_eval_map(int32_t n_classes, const int32_t* pred, const int32_t* tp, const int32_t* pos,
+                int32_t n_label_songs, double* map_out) {
+  if (!pred || !tp || !pos || !map_out || n_classes < 0) return mr_host::fail(MR_E_INVALID, "bad argument");
+  double total = 0.0;
+  for (int g = 0; g < n_classes; ++g) {
+    if (pos[g] <= 0) continue;  // AP = 0 for classes nobody holds
+    double P[10], R[10];
+    for (int t = 0; t < 10; ++t) {
+      const size_t i = (size_t)g * 10 + t;
+      P[t] = pred[i] > 0 ? (double)tp[i] / (double)pred[i] : 0.0;  // precision, MR:563-568
+      R[t] = (double)tp[i] / (double)pos[g];                        // recall, MR:576-581
+    }
+    double ap = 0.0;  // MR:601-609, summed left to right
+    for (int t = 0; t < 10; ++t) {
+      const double term = t == 9 ? 0.0 : t == 8 ? (R[8] - 0.0) * P[8] : (R[t] - R[t + 1]) * P[t];
+      ap = ap + term;
+    }
+    total += ap;
+  }
+  *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
+  return MR_OK;
+}
+
 }  // extern "C"

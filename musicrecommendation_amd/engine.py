@@ -134,6 +134,44 @@ class Engine:
                                                 None, out_songs_ptr, out_keys_ptr, out_scores_ptr or None),
                    "mr_topk_merge_device")
 
+    # ---- device-resident models (combination models, evaluation) -------------
+    def run_into(self, model: Union[str, int], dense_ptr: int) -> None:
+        """Asynchronous: like run(), the dense model written to a caller-owned
+        device buffer (n_test x width of this engine's dtype)."""
+        _lib.check(self._L.mr_run_into(self._h, model_id(model), ctypes.c_void_p(dense_ptr)), "mr_run_into")
+
+    def topk_dense(self, dense_ptr: int) -> None:
+        """Top-k of a dense device model into this engine's top-k outputs (read
+        them with topk()); synchronous."""
+        _lib.check(self._L.mr_topk_dense_device(self._h, ctypes.c_void_p(dense_ptr), self.topk_k),
+                   "mr_topk_dense_device")
+
+    def combine(self, kind: int, param: float, ubm_ptr: int, ibm_ptr: int, out_ptr: int, *, seed: int = 0,
+                pair_base: int = 0, n_pairs: int = 0) -> None:
+        """Combination model (MR:317-481) of two dense device models; synchronous."""
+        _lib.check(self._L.mr_combine_device(self._h, kind, float(param), int(seed) & (2 ** 64 - 1), int(pair_base),
+                                             int(n_pairs), ctypes.c_void_p(ubm_ptr), ctypes.c_void_p(ibm_ptr),
+                                             ctypes.c_void_p(out_ptr)), "mr_combine_device")
+
+    def eval_minmax(self, dense_ptr: int) -> Tuple[float, float]:
+        mn, mx = ctypes.c_double(), ctypes.c_double()
+        _lib.check(self._L.mr_eval_minmax_device(self._h, ctypes.c_void_p(dense_ptr), ctypes.byref(mn),
+                                                 ctypes.byref(mx)), "mr_eval_minmax_device")
+        return mn.value, mx.value
+
+    def eval_counts(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray,
+                    lab_songs: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """(pred, tp) counts, each width x 10 int32 (MR:529, MR:541-553)."""
+        lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
+        lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
+        pred = np.empty((self.width, 10), dtype=np.int32)
+        tp = np.empty((self.width, 10), dtype=np.int32)
+        _lib.check(self._L.mr_eval_counts_device(
+            self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
+            lab_songs.ctypes.data_as(ctypes.c_void_p), pred.ctypes.data_as(ctypes.c_void_p),
+            tp.ctypes.data_as(ctypes.c_void_p)), "mr_eval_counts_device")
+        return pred, tp
+
     def timing_begin(self) -> None:
         """Open a timing window (one event on the engine stream)."""
         _lib.check(self._L.mr_timing_begin(self._h), "mr_timing_begin")

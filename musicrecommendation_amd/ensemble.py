@@ -1,0 +1,153 @@
+"""Combination models and the reference's threshold mAP on the device.
+
+The reference builds three ensembles from the sorted ubm / ibm arrays
+(main.scala:57-59, MusicRecommender.scala MR:317-481) and scores every model
+with the threshold mAP of MR:521-639. Here both models stay on the GPU as
+dense [n_test x width] buffers (NaN = no pair); the combination, the min/max,
+the per-class confusion counts and the top-k run as HIP kernels
+(csrc/mr_ensemble.hip, csrc/mr_engine.hip k_topk_dense); the AP/mAP fold runs
+on the host over the integer counts (mr_eval_map).
+
+Multi-GPU: every rank holds one engine context (a song shard or a block of
+test users). min/max are all-reduced (MIN/MAX), the counts are all-reduced
+(SUM) into a full n_songs x 10 table, so every rank computes the same mAP,
+bit for bit, for any shard count.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from .engine import Engine
+
+LINEAR, AGGREGATION, STOCHASTIC = _lib.MR_COMB_LINEAR, _lib.MR_COMB_AGGREGATION, _lib.MR_COMB_STOCHASTIC
+_MASK = 2 ** 64 - 1
+
+
+def pair_uniform(seed: int, idx: int) -> float:
+    """The stochastic model's draw for pair `idx` (as mr_combine_device):
+    24 bits of splitmix64(seed + (idx+1)·0x9E3779B97F4A7C15) / 2^24 — the
+    distribution of java.util.Random.nextFloat (MR:414), seeded and
+    independent of launch geometry."""
+    z = (seed + (idx + 1) * 0x9E3779B97F4A7C15) & _MASK
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _MASK
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _MASK
+    z ^= z >> 31
+    return float(np.float32(z >> 40) * np.float32(1.0 / 16777216.0))
+
+
+def eval_map(pred: np.ndarray, tp: np.ndarray, pos: np.ndarray, n_label_songs: int) -> float:
+    """mAP from the per-class counts (mr_eval_map, MR:588-627)."""
+    pred = np.ascontiguousarray(pred, dtype=np.int32)
+    tp = np.ascontiguousarray(tp, dtype=np.int32)
+    pos = np.ascontiguousarray(pos, dtype=np.int32)
+    out = ctypes.c_double()
+    _lib.check(_lib.lib().mr_eval_map(pred.shape[0], pred.ctypes.data_as(ctypes.c_void_p),
+                                      tp.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p),
+                                      int(n_label_songs), ctypes.byref(out)), "mr_eval_map")
+    return out.value
+
+
+class DeviceEnsemble:
+    """Dense models of one engine context as torch device tensors.
+
+    pair_base / n_pairs place this context's pairs in the full model's
+    (user, song) order (aggregation threshold and stochastic draws); pos /
+    n_label_songs are the GLOBAL per-class label counts (defaults: this
+    context's dataset, i.e. a single-process run)."""
+
+    def __init__(self, engine: Engine, *, pair_base: int = 0, n_pairs: Optional[int] = None,
+                 pos: Optional[np.ndarray] = None, n_label_songs: Optional[int] = None, group=None):
+        import torch
+
+        from . import evaluation
+
+        self.e = engine
+        self.ds = engine.dataset
+        self.device = torch.device("cuda", engine.opt.device)
+        self.torch_dtype = torch.float64 if engine.dtype == np.float64 else torch.float32
+        self.shape = (engine.n_test, engine.width)
+        self.pair_base = int(pair_base)
+        self.n_pairs = int(n_pairs if n_pairs is not None else self.ds.n_pairs())
+        self.pos = evaluation.label_pos(self.ds) if pos is None else np.asarray(pos, dtype=np.int32)
+        self.n_label_songs = int(self.ds.n_label_songs if n_label_songs is None else n_label_songs)
+        self.group = group
+
+    def empty(self):
+        import torch
+
+        return torch.empty(self.shape, dtype=self.torch_dtype, device=self.device)
+
+    # ---- models ----------------------------------------------------------------
+    def model(self, name: str):
+        """ubm / ibm dense model (MR:132-307) into a new device tensor."""
+        import torch
+
+        t = self.empty()
+        torch.cuda.synchronize(self.device)  # allocation visible before the engine stream writes it
+        self.e.run_into(name, t.data_ptr())
+        self.e.sync()
+        return t
+
+    def _combine(self, kind: int, ubm, ibm, param: float, seed: int = 0):
+        out = self.empty()
+        self.e.combine(kind, param, ubm.data_ptr(), ibm.data_ptr(), out.data_ptr(), seed=seed,
+                       pair_base=self.pair_base, n_pairs=self.n_pairs)
+        return out
+
+    def linear(self, ubm, ibm, alpha: float):
+        """getLinearCombinationModel (MR:317-351)."""
+        return self._combine(LINEAR, ubm, ibm, alpha)
+
+    def aggregation(self, ubm, ibm, item_based_percentage: float = 0.5):
+        """getAggregationModel (MR:361-418)."""
+        return self._combine(AGGREGATION, ubm, ibm, item_based_percentage)
+
+    def stochastic(self, ubm, ibm, item_based_probability: float = 0.5, seed: int = 0):
+        """getStochasticCombinationModel (MR:429-481), seeded."""
+        return self._combine(STOCHASTIC, ubm, ibm, item_based_probability, seed)
+
+    # ---- evaluation --------------------------------------------------------------
+    def _world(self) -> int:
+        import torch.distributed as dist
+
+        return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+
+    def threshold_map(self, t) -> float:
+        """evaluateModel (MR:636) of a dense device model."""
+        import torch
+        import torch.distributed as dist
+
+        mn, mx = self.e.eval_minmax(t.data_ptr())
+        world = self._world()
+        if world > 1:
+            be = dist.get_backend(self.group)
+            dev = self.device if be == "nccl" else torch.device("cpu")
+            a = torch.tensor([mn], dtype=torch.float64, device=dev)
+            b = torch.tensor([mx], dtype=torch.float64, device=dev)
+            dist.all_reduce(a, op=dist.ReduceOp.MIN, group=self.group)
+            dist.all_reduce(b, op=dist.ReduceOp.MAX, group=self.group)
+            mn, mx = float(a.item()), float(b.item())
+        if not (mn <= mx):
+            raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
+        pred, tp = self.e.eval_counts(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs)
+        full_p = np.zeros((self.ds.n_songs, 10), dtype=np.int32)
+        full_t = np.zeros_like(full_p)
+        full_p[self.e.song_lo:self.e.song_hi] = pred
+        full_t[self.e.song_lo:self.e.song_hi] = tp
+        if world > 1:
+            be = dist.get_backend(self.group)
+            dev = self.device if be == "nccl" else torch.device("cpu")
+            c = torch.from_numpy(np.stack([full_p, full_t])).to(dev)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+            c = c.cpu().numpy()
+            full_p, full_t = c[0], c[1]
+        return eval_map(full_p, full_t, self.pos, self.n_label_songs)
+
+    def topk(self, t) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Top-k recommendation lists of a dense device model (k = engine topk)."""
+        self.e.topk_dense(t.data_ptr())
+        return self.e.topk()

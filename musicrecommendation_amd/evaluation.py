@@ -26,28 +26,44 @@ def label_matrix(ds: Dataset) -> np.ndarray:
     return m
 
 
-def threshold_map(scores: np.ndarray, ds: Dataset, thresholds=THRESHOLDS) -> float:
-    """Reference threshold mAP of a dense model (MR:636)."""
+def label_pos(ds: Dataset) -> np.ndarray:
+    """pos[s] = #test users whose labels hold song s (TP + FN of class s), s < n_songs."""
+    keep = ds.lab_songs < ds.n_songs
+    return np.bincount(ds.lab_songs[keep], minlength=ds.n_songs).astype(np.int32)
+
+
+def threshold_counts(scores: np.ndarray, ds: Dataset, mn: float, mx: float, thresholds=THRESHOLDS):
+    """(pred, tp), each n_songs x 10: per song and threshold, the test users
+    predicted ((x - mn)/(mx - mn) > t, MR:529) and those of them whose labels
+    hold the song (MR:541-553). The numpy twin of mr_eval_counts_device."""
     x = np.asarray(scores, dtype=np.float64)
     valid = ~np.isnan(x)
-    if ds.n_label_songs == 0:
-        return float("nan")
-    mn = x[valid].min()
-    mx = x[valid].max()
     with np.errstate(invalid="ignore", divide="ignore"):
         norm = (x - mn) / (mx - mn)
     lab = label_matrix(ds)
-    pos = lab.sum(axis=0)                      # TP + FN per song
-    P, R = [], []
-    for t in thresholds:
+    pred = np.zeros((x.shape[1], len(thresholds)), dtype=np.int64)
+    tp = np.zeros_like(pred)
+    for i, t in enumerate(thresholds):
         with np.errstate(invalid="ignore"):
-            pred = valid & (norm > t)          # NaN > t is False (MR:529)
-        tp = (pred & lab).sum(axis=0)
-        pp = pred.sum(axis=0)                  # TP + FP
-        P.append(np.where(pp > 0, tp / np.maximum(pp, 1), 0.0))
-        R.append(np.where(pos > 0, tp / np.maximum(pos, 1), 0.0))
-    n = len(thresholds)
-    ap = np.zeros(ds.n_songs)
+            p = valid & (norm > t)             # NaN > t is False (MR:529)
+        pred[:, i] = p.sum(axis=0)
+        tp[:, i] = (p & lab).sum(axis=0)
+    return pred, tp
+
+
+def map_from_counts(pred: np.ndarray, tp: np.ndarray, pos: np.ndarray, n_label_songs: int) -> float:
+    """AP per class (MR:588-618) and the mean (MR:625-627) from the counts:
+    P_i = TP/(TP+FP), R_i = TP/(TP+FN) (MR:563-581), AP = Σ_{i<8} (R_i−R_{i+1})·P_i
+    + R_8·P_8 + 0 (left fold), classes summed in song-id order."""
+    if n_label_songs == 0:
+        return float("nan")
+    pred = np.asarray(pred, dtype=np.float64)
+    tp = np.asarray(tp, dtype=np.float64)
+    pos = np.asarray(pos)
+    n = pred.shape[1]
+    P = [np.where(pred[:, i] > 0, tp[:, i] / np.maximum(pred[:, i], 1), 0.0) for i in range(n)]
+    R = [np.where(pos > 0, tp[:, i] / np.maximum(pos, 1), 0.0) for i in range(n)]
+    ap = np.zeros(pred.shape[0])
     for i in range(n):                         # List.sum: left fold in threshold order
         if i == n - 1:
             term = 0.0
@@ -56,11 +72,22 @@ def threshold_map(scores: np.ndarray, ds: Dataset, thresholds=THRESHOLDS) -> flo
         else:
             term = (R[i] - R[i + 1]) * P[i]
         ap = ap + term
-    cls = pos > 0                              # other newSongs have AP = 0
     total = 0.0
-    for v in ap[cls]:
+    for v in ap[pos > 0]:                      # other newSongs have AP = 0
         total += float(v)
-    return total / ds.n_label_songs
+    return total / n_label_songs
+
+
+def threshold_map(scores: np.ndarray, ds: Dataset, thresholds=THRESHOLDS) -> float:
+    """Reference threshold mAP of a dense model (MR:636), on the host."""
+    x = np.asarray(scores, dtype=np.float64)
+    valid = ~np.isnan(x)
+    if ds.n_label_songs == 0:
+        return float("nan")
+    mn = x[valid].min()
+    mx = x[valid].max()
+    pred, tp = threshold_counts(x, ds, mn, mx, thresholds)
+    return map_from_counts(pred, tp, label_pos(ds), ds.n_label_songs)
 
 
 def map_at_k(top_songs: np.ndarray, ds: Dataset, k: int = 10) -> float:

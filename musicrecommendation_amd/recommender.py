@@ -101,10 +101,69 @@ class MusicRecommender:
         """main.scala:57-59 ordering: (user, song, -score)."""
         return sorted(model, key=lambda t: (t[0], t[1][0], -t[1][1]))
 
+    # ---- combination models (MR:317-481) ------------------------------------------
+    # Over the Model arrays, in the order given (the driver passes them sorted
+    # by (user, song), main.scala:57-59). Mismatched pairs: the reference calls
+    # System.exit(2) (MR:326); a bad percentage: System.exit(-1) (MR:366-369).
+    # Both raise ValueError here. On-device versions over dense models:
+    # ensemble.DeviceEnsemble (the C5 path).
+    @staticmethod
+    def _zip(ubm: Model, ibm: Model):
+        if len(ubm) != len(ibm):
+            raise ValueError("ubm and ibm differ in length (reference: System.exit(2), MR:326)")
+        for (u1, (s1, r1)), (u2, (s2, r2)) in zip(ubm, ibm):
+            if u1 != u2 or s1 != s2:
+                raise ValueError(f"pair mismatch ({u1},{s1}) vs ({u2},{s2}) (reference: System.exit(2), MR:326)")
+            yield u1, s1, r1, r2
+
+    @staticmethod
+    def _check_fraction(x: float, what: str) -> None:
+        if x < 0 or x > 1:
+            raise ValueError(f"{what} must be between 0 and 1 (reference: System.exit(-1), MR:366-369)")
+
+    def getLinearCombinationModel(self, ubm: Model, ibm: Model, alpha: float) -> Model:
+        return [(u, (s, r1 * alpha + r2 * (1 - alpha))) for u, s, r1, r2 in self._zip(ubm, ibm)]
+
+    def getLinearCombinationModelP(self, ubm: Model, ibm: Model, alpha: float) -> Model:
+        return self.getLinearCombinationModel(ubm, ibm, alpha)
+
+    def getAggregationModel(self, ubm: Model, ibm: Model, itemBasedPercentage: float = 0.5) -> Model:
+        self._check_fraction(itemBasedPercentage, "Percentage")
+        threshold = int(itemBasedPercentage * len(ubm))
+        return [(u, (s, r2 if i < threshold else r1)) for i, (u, s, r1, r2) in enumerate(self._zip(ubm, ibm))]
+
+    def getAggregationModelP(self, ubm: Model, ibm: Model, itemBasedPercentage: float = 0.5) -> Model:
+        return self.getAggregationModel(ubm, ibm, itemBasedPercentage)
+
+    def getStochasticCombinationModel(self, ubm: Model, ibm: Model, itemBasedProbability: float = 0.5,
+                                      seed: int = 0) -> Model:
+        """The reference draws from an unseeded java.util.Random (MR:439); here
+        the draw of the i-th pair is ensemble.pair_uniform(seed, i), the stream
+        the device kernel uses, so list and device results agree."""
+        from .ensemble import pair_uniform
+
+        self._check_fraction(itemBasedProbability, "Probability")
+        return [(u, (s, r2 if pair_uniform(seed, i) < itemBasedProbability else r1))
+                for i, (u, s, r1, r2) in enumerate(self._zip(ubm, ibm))]
+
+    def getStochasticCombinationModelP(self, ubm: Model, ibm: Model, itemBasedProbability: float = 0.5,
+                                       seed: int = 0) -> Model:
+        return self.getStochasticCombinationModel(ubm, ibm, itemBasedProbability, seed)
+
     # ---- evaluation (MR:636-639) ------------------------------------------------
     def evaluateModel(self, model: Union[Model, np.ndarray], parallel: bool = False) -> float:
+        """Threshold mAP (MR:636) on the device: the model goes to HBM as a
+        dense buffer, min/max + confusion counts run as HIP kernels."""
+        import torch
+
+        from .ensemble import DeviceEnsemble
+
         dense = model if isinstance(model, np.ndarray) else self._from_model(model)
-        return evaluation.threshold_map(dense, self.dataset)
+        eng = self.engine()
+        ens = DeviceEnsemble(eng)
+        t = torch.from_numpy(np.ascontiguousarray(dense, dtype=eng.dtype)).to(ens.device)
+        torch.cuda.synchronize(ens.device)
+        return ens.threshold_map(t)
 
     def _from_model(self, model: Model) -> np.ndarray:
         ds = self.dataset

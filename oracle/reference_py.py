@@ -134,6 +134,30 @@ class LiteralRecommender:
             out.append((u1, (s1, r2)) if idx < threshold else (u1, (s1, r1)))
         return out
 
+    # MR:429-452 with the reference's unseeded java.util.Random replaced by the
+    # build's seeded stream (restated here from include/mr_engine.h
+    # MR_COMB_STOCHASTIC: 24 bits of splitmix64(seed + (i+1)*golden) / 2^24).
+    @staticmethod
+    def uniform(seed: int, idx: int) -> float:
+        m = (1 << 64) - 1
+        z = (seed + (idx + 1) * 0x9E3779B97F4A7C15) & m
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+        z ^= z >> 31
+        return (z >> 40) / 16777216.0  # exact in float32 and float64
+
+    @staticmethod
+    def stochastic(ubm: Model, ibm: Model, item_based_probability: float = 0.5, seed: int = 0) -> Model:
+        if item_based_probability < 0 or item_based_probability > 1:
+            raise SystemExit(-1)
+        out: Model = []
+        for idx, ((u1, (s1, r1)), (u2, (s2, r2))) in enumerate(zip(ubm, ibm)):
+            if u1 != u2 or s1 != s2:
+                raise SystemExit(2)
+            take = LiteralRecommender.uniform(seed, idx) < item_based_probability
+            out.append((u1, (s1, r2)) if take else (u1, (s1, r1)))
+        return out
+
     # ---- evaluation, MR:521-639 ----
     @staticmethod
     def prediction_to_class_labels(model: Model, threshold: float) -> Dict[str, List[str]]:
