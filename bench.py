@@ -135,6 +135,82 @@ def cpu_baseline_twohop(ds, model: str, seconds: float):
     }
 
 
+def run_c5(args, world: int, rank: int, local: int) -> None:
+    """Config 5: the reference's whole evaluation pipeline on device — ubm + ibm
+    dense models, linear / aggregation / stochastic combinations (main.scala:57-89,
+    MR:317-481) and the threshold mAP of all five (MR:636), 2,000 test users
+    against the full train set. N > 1: song-range shards (the north star's
+    layout); combinations are per pair, the mAP reductions go over RCCL."""
+    from musicrecommendation_amd import evaluation
+    from musicrecommendation_amd.ensemble import DeviceEnsemble
+    from musicrecommendation_amd.sharding import song_shards
+
+    n_tr, n_te, _seed = synth.BULK_CONFIGS["c5"]
+    ds = synth.config("c5").dataset()
+    lo, hi = song_shards(ds, world)[rank] if world > 1 else (0, ds.n_songs)
+    eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi)
+    ens = DeviceEnsemble(eng, pos=evaluation.label_pos(ds), n_label_songs=ds.n_label_songs)
+    maps = {}
+
+    def step():
+        ubm, ibm = ens.model("ubm"), ens.model("ibm")
+        models = {"ubm": ubm, "ibm": ibm, "lcm": ens.linear(ubm, ibm, 0.5), "am": ens.aggregation(ubm, ibm, 0.5),
+                  "scm": ens.stochastic(ubm, ibm, 0.5, seed=1)}
+        for name, t in models.items():
+            maps[name] = ens.threshold_map(t)
+        return models
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        models = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+    if rank == 0:
+        pairs = ds.n_pairs()
+        value = pairs * args.steps / elapsed
+        songs, _sc, _k = ens.topk(models["lcm"])  # this rank's shard when world > 1
+        ab = algorithmic_bytes(ds, 4, 10)
+        model_bytes = sum(ab.values())
+        dense_elems = ds.n_test * ds.n_songs
+        # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)
+        step_bytes = 2 * model_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
+        step_s = elapsed / args.steps
+        line = {
+            "metric": "scored (test-user,song) pairs/sec, ensemble ubm+ibm+lcm+am+scm + threshold mAP",
+            "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (bulk Zipf/lognormal Taste-Profile-shaped triplets, capped head, SURVEY.md §8d)",
+            "config": {"workload": f"c5: {n_tr} train / {n_te} test / {ds.n_songs} songs; ubm + ibm dense fp32, "
+                                   f"linear(0.5) + aggregation(0.5) + stochastic(0.5, seed 1), threshold mAP x5",
+                       "n_train": n_tr, "n_test": n_te, "n_songs": ds.n_songs, "pairs_per_step": pairs,
+                       "parallelism": f"songs{world}"},
+            "roofline": {"bound": "hbm", "kernel": "whole step (2 scoring passes + 3 combinations + 5 evaluations)",
+                         "achieved": step_bytes / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_step": step_bytes},
+            "threshold_mAP": maps,
+            "mAP@10_lcm": evaluation.map_at_k(songs, ds, 10) if world == 1 else None,
+            "cpu_baseline": (cpu_baseline_twohop(ds, "ibm", args.cpu_baseline_seconds)
+                             if world == 1 and not args.no_cpu_baseline else None),
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,6 +237,9 @@ def main() -> None:
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.config == "c5":
+        run_c5(args, world, rank, local)
+        return
     bulk = args.config in synth.BULK_CONFIGS
     if bulk:  # full-scale: fixed test set, top-k only (SURVEY.md §8d OUT = 12k)
         n_tr, n_te, _seed = synth.BULK_CONFIGS[args.config]
