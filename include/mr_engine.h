@@ -292,6 +292,23 @@ int mr_corpus_labels(const mr_corpus* c, const int64_t** off, const int32_t** so
 const char* mr_corpus_name(const mr_corpus* c, int32_t kind, int32_t id);
 int mr_corpus_free(mr_corpus* c);
 
+/* ---- model files (MR:489-512) --------------------------------------------
+ * writeModelOnFile (MR:489-497): one "user\tsong\tscore\n" line per pair of a
+ * dense n_test x n_songs model (NaN = no pair), the score formatted as
+ * java.lang.Double.toString (shortest round-trip digits, JDK 19+). order 0 =
+ * getModel's emission order (song-major, MR:106-108), 1 = the driver's sorted
+ * (user, song) order (main.scala:57-59, names sorted like their ids). */
+int mr_model_write_tsv(const char* path, int32_t n_test, int32_t n_songs, const char* const* user_names,
+                       const char* const* song_names, const double* dense, int32_t order);
+/* importModelFromFile (MR:505-512) into a dense n_test x n_songs buffer over
+ * the given names (NaN where the file has no line). Malformed line ->
+ * MR_E_PARSE (the reference: MatchError / NumberFormatException); unknown
+ * name or duplicate pair -> MR_E_INVALID. */
+int mr_model_read_tsv(const char* path, int32_t n_test, int32_t n_songs, const char* const* user_names,
+                      const char* const* song_names, double* dense);
+/* java.lang.Double.toString(x) into buf; returns its length (or an error code). */
+int mr_java_double_string(double x, char* buf, int32_t cap);
+
 /* Library version string. */
 const char* mr_version(void);
 

@@ -138,6 +138,9 @@ SIGNATURES = {
     "mr_corpus_name": (c_char_p, [c_void_p, c_int32, c_int32]),
     "mr_corpus_free": (c_int, [c_void_p]),
     "mr_version": (c_char_p, []),
+    "mr_model_write_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32]),
+    "mr_model_read_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "mr_java_double_string": (c_int, [c_double, c_char_p, c_int32]),
 }
 
 _lib = None

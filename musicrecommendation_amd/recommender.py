@@ -150,6 +150,24 @@ class MusicRecommender:
                                        seed: int = 0) -> Model:
         return self.getStochasticCombinationModel(ubm, ibm, itemBasedProbability, seed)
 
+    # ---- model files (MR:489-512) --------------------------------------------------
+    @staticmethod
+    def writeModelOnFile(model: Model, outputFileName: str) -> None:
+        """One "user\tsong\tscore" line per element, in the given order, the
+        score as java.lang.Double.toString (MR:489-497)."""
+        from .modelio import java_double_string
+
+        with open(outputFileName, "w") as f:
+            for u, (s, x) in model:
+                f.write(f"{u}\t{s}\t{java_double_string(x)}\n")
+
+    @staticmethod
+    def importModelFromFile(pathToModel: str):
+        """(user, song, score) triplets sorted by (user, song, -score) (MR:505-512)."""
+        from .modelio import import_model
+
+        return import_model(pathToModel)
+
     # ---- evaluation (MR:636-639) ------------------------------------------------
     def evaluateModel(self, model: Union[Model, np.ndarray], parallel: bool = False) -> float:
         """Threshold mAP (MR:636) on the device: the model goes to HBM as a
