@@ -1,5 +1,5 @@
 // mr_host.cpp — host-side part of the engine's C ABI (no GPU needed):
-//  * TSV ingest + string interning + CSR build, replacing extractData /
+//  * parallel TSV ingest + string interning + CSR build, replacing extractData /
 //    songs / songsToUsersMap / importTestLabels (MusicRecommender.scala MR:26-91);
 //  * the per-shard top-k merge on the host (exchange step of a song-sharded run).
 #include <algorithm>
@@ -7,8 +7,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <fstream>
 #include <string>
+#include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -22,17 +23,118 @@ int fail(int code, const char* fmt, ...);
 
 namespace {
 
+// ---- parallel TSV reader -------------------------------------------------------
+// The whole file is read into memory and cut into per-thread chunks at line
+// starts; every thread splits its lines (Java String.split("\t") semantics:
+// trailing empty fields dropped, then exactly 3 fields, MR:34-35) into string
+// views and interns user / song names in thread-local tables. The tables are
+// merged afterwards (distinct names only), so the hot loop touches no shared
+// state.
+using sv = std::string_view;
+
+int read_file(const char* path, std::vector<char>& out) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return mr_host::fail(MR_E_IO, "cannot open %s", path);
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  if (n < 0) { std::fclose(f); return mr_host::fail(MR_E_IO, "cannot size %s", path); }
+  out.resize((size_t)n);
+  const size_t got = n ? std::fread(out.data(), 1, (size_t)n, f) : 0;
+  std::fclose(f);
+  if (got != (size_t)n) return mr_host::fail(MR_E_IO, "short read of %s", path);
+  return MR_OK;
+}
+
+struct Local {  // one thread's share of one file
+  std::unordered_map<sv, int> uid, sid;
+  std::vector<sv> unames, snames;
+  std::vector<int> ru, rs;
+  size_t err_off = SIZE_MAX;
+  int err_fields = 0;
+};
+
+void parse_chunk(const char* p, size_t a, size_t b, Local& c) {
+  size_t i = a;
+  while (i < b) {
+    const char* nl = static_cast<const char*>(std::memchr(p + i, '\n', b - i));
+    const size_t end = nl ? (size_t)(nl - p) : b;
+    size_t le = end;
+    if (le > i && p[le - 1] == '\r') --le;  // getLines strips \r\n
+    int nf = 0, last_ne = -1;
+    sv f0, f1;
+    size_t s = i;
+    while (true) {
+      const char* t = static_cast<const char*>(std::memchr(p + s, '\t', le - s));
+      const size_t fe = t ? (size_t)(t - p) : le;
+      if (fe > s) last_ne = nf;
+      if (nf == 0) f0 = sv(p + s, fe - s);
+      else if (nf == 1) f1 = sv(p + s, fe - s);
+      ++nf;
+      if (!t) break;
+      s = fe + 1;
+    }
+    if (last_ne + 1 != 3) {  // scala.MatchError (MR:34)
+      c.err_off = i;
+      c.err_fields = last_ne + 1;
+      return;
+    }
+    auto u = c.uid.try_emplace(f0, (int)c.unames.size());
+    if (u.second) c.unames.push_back(f0);
+    auto so = c.sid.try_emplace(f1, (int)c.snames.size());
+    if (so.second) c.snames.push_back(f1);
+    c.ru.push_back(u.first->second);
+    c.rs.push_back(so.first->second);
+    i = nl ? end + 1 : b;
+  }
+}
+
+int n_threads() {
+  const char* e = std::getenv("MR_INGEST_THREADS");
+  int t = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(t, 32));
+}
+
+int parse_file(const char* path, const std::vector<char>& text, std::vector<Local>& parts) {
+  const size_t n = text.size();
+  // chunks of >= 1 MiB (MR_INGEST_MIN_CHUNK overrides, e.g. to split small files in tests)
+  const char* mc = std::getenv("MR_INGEST_MIN_CHUNK");
+  const size_t min_chunk = mc ? std::max<size_t>(1, (size_t)std::atoll(mc)) : ((size_t)1 << 20);
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_threads(), n / min_chunk + 1));
+  std::vector<size_t> cut(T + 1, n);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    size_t x = std::max(cut[t - 1], n * t / T);
+    while (x < n && x > 0 && text[x - 1] != '\n') ++x;
+    cut[t] = x;
+  }
+  parts.assign(T, Local());
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    parts[t].ru.reserve((cut[t + 1] - cut[t]) / 48 + 16);
+    parts[t].rs.reserve((cut[t + 1] - cut[t]) / 48 + 16);
+    th.emplace_back(parse_chunk, text.data(), cut[t], cut[t + 1], std::ref(parts[t]));
+  }
+  for (auto& x : th) x.join();
+  size_t bad = SIZE_MAX;
+  int fields = 0;
+  for (auto& c : parts)
+    if (c.err_off < bad) { bad = c.err_off; fields = c.err_fields; }
+  if (bad != SIZE_MAX) {
+    const size_t lineno = 1 + (size_t)std::count(text.begin(), text.begin() + (long)bad, '\n');
+    return mr_host::fail(MR_E_PARSE, "%s:%zu: expected 3 tab-separated fields, got %d", path, lineno, fields);
+  }
+  return MR_OK;
+}
+
 struct Table {
   // interning in first-seen order, re-numbered lexicographically at the end
-  std::unordered_map<std::string, int> id;
-  std::vector<std::string> names;
-  int get(const std::string& s) {
-    auto it = id.find(s);
-    if (it != id.end()) return it->second;
-    int k = (int)names.size();
-    id.emplace(s, k);
-    names.push_back(s);
-    return k;
+  std::unordered_map<sv, int> id;
+  std::vector<sv> names;
+  int get(sv s) {
+    auto it = id.try_emplace(s, (int)names.size());
+    if (it.second) names.push_back(s);
+    return it.first->second;
   }
   // old id -> new lexicographic id
   std::vector<int> lex_order() const {
@@ -50,31 +152,20 @@ struct Row {
   int song;
 };
 
-// Split like Java's String.split("\t"): trailing empty fields are dropped;
-// the reference then pattern-matches exactly three fields (MR:34-35).
-int parse_file(const char* path, std::vector<std::pair<std::string, std::string>>& out) {
-  std::ifstream in(path, std::ios::binary);
-  if (!in) return mr_host::fail(MR_E_IO, "cannot open %s", path);
-  std::string line;
-  size_t lineno = 0;
-  std::vector<std::string> f;
-  while (std::getline(in, line)) {
-    ++lineno;
-    if (!line.empty() && line.back() == '\r') line.pop_back();  // getLines strips \r\n
-    f.clear();
-    size_t a = 0;
-    while (true) {
-      size_t b = line.find('\t', a);
-      if (b == std::string::npos) { f.emplace_back(line.substr(a)); break; }
-      f.emplace_back(line.substr(a, b - a));
-      a = b + 1;
-    }
-    while (!f.empty() && f.back().empty()) f.pop_back();
-    if (f.size() != 3)
-      return mr_host::fail(MR_E_PARSE, "%s:%zu: expected 3 tab-separated fields, got %zu", path, lineno, f.size());
-    out.emplace_back(std::move(f[0]), std::move(f[1]));
+// Merge the per-thread tables of one file into the global user / song tables
+// and append its rows (global first-seen ids).
+void merge_parts(std::vector<Local>& parts, Table& users, Table& songs, std::vector<Row>& rows) {
+  size_t total = 0;
+  for (auto& c : parts) total += c.ru.size();
+  rows.reserve(rows.size() + total);
+  for (auto& c : parts) {
+    std::vector<int> ug(c.unames.size()), sg(c.snames.size());
+    for (size_t i = 0; i < ug.size(); ++i) ug[i] = users.get(c.unames[i]);
+    for (size_t i = 0; i < sg.size(); ++i) sg[i] = songs.get(c.snames[i]);
+    for (size_t r = 0; r < c.ru.size(); ++r) rows.push_back({ug[c.ru[r]], sg[c.rs[r]]});
+    std::vector<int>().swap(c.ru);
+    std::vector<int>().swap(c.rs);
   }
-  return MR_OK;
 }
 
 }  // namespace
@@ -90,20 +181,27 @@ struct mr_corpus {
 
 namespace {
 
-// Build CSR rows (sorted unique) + duplicate-counting lengths.
+// Build CSR rows (sorted unique) + duplicate-counting lengths: counting sort
+// by user, then sort + unique inside each row.
 void build_rows(int n_users, const std::vector<Row>& rows, std::vector<int64_t>& off,
                 std::vector<int32_t>& col, std::vector<int32_t>* len) {
-  std::vector<std::vector<int32_t>> per(n_users);
-  for (const Row& r : rows) per[r.user].push_back(r.song);
-  off.assign(n_users + 1, 0);
+  std::vector<int64_t> start((size_t)n_users + 1, 0);
+  for (const Row& r : rows) start[(size_t)r.user + 1]++;
+  for (int u = 0; u < n_users; ++u) start[u + 1] += start[u];
+  std::vector<int32_t> tmp(rows.size());
+  {
+    std::vector<int64_t> cur(start.begin(), start.end() - 1);
+    for (const Row& r : rows) tmp[cur[r.user]++] = r.song;
+  }
+  off.assign((size_t)n_users + 1, 0);
   if (len) len->assign(n_users, 0);
   col.clear();
+  col.reserve(rows.size());
   for (int u = 0; u < n_users; ++u) {
-    auto& v = per[u];
-    if (len) (*len)[u] = (int32_t)v.size();
-    std::sort(v.begin(), v.end());
-    v.erase(std::unique(v.begin(), v.end()), v.end());
-    col.insert(col.end(), v.begin(), v.end());
+    auto b = tmp.begin() + start[u], e = tmp.begin() + start[u + 1];
+    if (len) (*len)[u] = (int32_t)(e - b);
+    std::sort(b, e);
+    col.insert(col.end(), b, std::unique(b, e));
     off[u + 1] = (int64_t)col.size();
   }
 }
@@ -116,31 +214,32 @@ int mr_corpus_from_tsv(const char* train_path, const char* test_path, const char
                        mr_corpus** out) {
   if (!train_path || !test_path || !out) return mr_host::fail(MR_E_INVALID, "null argument");
   *out = nullptr;
-  std::vector<std::pair<std::string, std::string>> tr, te, lab;
+  std::vector<char> tr_text, te_text, lab_text;
+  std::vector<Local> tr, te, lab;
   int rc;
-  if ((rc = parse_file(train_path, tr))) return rc;
-  if ((rc = parse_file(test_path, te))) return rc;
-  if (labels_path && (rc = parse_file(labels_path, lab))) return rc;
+  if ((rc = read_file(train_path, tr_text)) || (rc = parse_file(train_path, tr_text, tr))) return rc;
+  if ((rc = read_file(test_path, te_text)) || (rc = parse_file(test_path, te_text, te))) return rc;
+  if (labels_path && ((rc = read_file(labels_path, lab_text)) || (rc = parse_file(labels_path, lab_text, lab))))
+    return rc;
 
   Table songs, trainU, testU;
   std::vector<Row> tr_rows, te_rows;
-  tr_rows.reserve(tr.size());
-  te_rows.reserve(te.size());
-  for (auto& l : tr) tr_rows.push_back({trainU.get(l.first), songs.get(l.second)});
-  for (auto& l : te) te_rows.push_back({testU.get(l.first), songs.get(l.second)});
+  merge_parts(tr, trainU, songs, tr_rows);
+  merge_parts(te, testU, songs, te_rows);
   for (auto& kv : testU.id)
     if (trainU.id.count(kv.first))
-      return mr_host::fail(MR_E_INVALID, "user %s is in both the train and the test file", kv.first.c_str());
+      return mr_host::fail(MR_E_INVALID, "user %s is in both the train and the test file",
+                           std::string(kv.first).c_str());
 
   auto* c = new mr_corpus();
   const std::vector<int> srm = songs.lex_order(), trm = trainU.lex_order(), term = testU.lex_order();
   c->n_songs = (int)songs.names.size();
   c->song_names.resize(c->n_songs);
-  for (size_t i = 0; i < srm.size(); ++i) c->song_names[srm[i]] = songs.names[i];
+  for (size_t i = 0; i < srm.size(); ++i) c->song_names[srm[i]] = std::string(songs.names[i]);
   c->train_names.resize(trm.size());
-  for (size_t i = 0; i < trm.size(); ++i) c->train_names[trm[i]] = trainU.names[i];
+  for (size_t i = 0; i < trm.size(); ++i) c->train_names[trm[i]] = std::string(trainU.names[i]);
   c->test_names.resize(term.size());
-  for (size_t i = 0; i < term.size(); ++i) c->test_names[term[i]] = testU.names[i];
+  for (size_t i = 0; i < term.size(); ++i) c->test_names[term[i]] = std::string(testU.names[i]);
   c->song_count.assign(c->n_songs, 0);
   for (auto& r : tr_rows) { r.user = trm[r.user]; r.song = srm[r.song]; c->song_count[r.song]++; }
   for (auto& r : te_rows) { r.user = term[r.user]; r.song = srm[r.song]; c->song_count[r.song]++; }
@@ -151,25 +250,24 @@ int mr_corpus_from_tsv(const char* train_path, const char* test_path, const char
   // label songs outside `songs` are numbered after them lexicographically.
   Table extra;
   std::vector<Row> lab_rows;
-  std::unordered_map<std::string, int> label_song_set;
-  std::unordered_map<std::string, int> song_id;
-  song_id.reserve(c->song_names.size());
-  for (int s = 0; s < c->n_songs; ++s) song_id.emplace(c->song_names[s], s);
-  std::vector<std::pair<int, std::string>> pending;  // (test user, extra song name)
-  for (auto& l : lab) {
-    label_song_set.emplace(l.second, 1);
-    auto tu = testU.id.find(l.first);
-    auto si = song_id.find(l.second);
-    if (si == song_id.end()) extra.get(l.second);
-    if (tu == testU.id.end()) continue;  // never looked up by the reference (MR:545)
-    if (si != song_id.end()) lab_rows.push_back({term[tu->second], si->second});
-    else pending.emplace_back(term[tu->second], l.second);
-  }
+  std::unordered_map<sv, int> label_song_set;
+  std::vector<std::pair<int, sv>> pending;  // (test user, extra song name)
+  for (auto& part : lab)
+    for (size_t r = 0; r < part.ru.size(); ++r) {
+      const sv un = part.unames[part.ru[r]], sn = part.snames[part.rs[r]];
+      label_song_set.emplace(sn, 1);
+      auto tu = testU.id.find(un);
+      auto si = songs.id.find(sn);
+      if (si == songs.id.end()) extra.get(sn);
+      if (tu == testU.id.end()) continue;  // never looked up by the reference (MR:545)
+      if (si != songs.id.end()) lab_rows.push_back({term[tu->second], srm[si->second]});
+      else pending.emplace_back(term[tu->second], sn);
+    }
   const std::vector<int> erm = extra.lex_order();
   c->n_extra = (int)extra.names.size();
   c->song_names.resize(c->n_songs + c->n_extra);
-  for (size_t i = 0; i < erm.size(); ++i) c->song_names[c->n_songs + erm[i]] = extra.names[i];
-  for (auto& p : pending) lab_rows.push_back({p.first, c->n_songs + erm[extra.id[p.second]]});
+  for (size_t i = 0; i < erm.size(); ++i) c->song_names[c->n_songs + erm[i]] = std::string(extra.names[i]);
+  for (auto& pr : pending) lab_rows.push_back({pr.first, c->n_songs + erm[extra.id[pr.second]]});
   c->n_label_songs = (int)label_song_set.size();
   build_rows((int)c->test_names.size(), lab_rows, c->lab_off, c->lab_songs, nullptr);
   *out = c;

@@ -91,3 +91,27 @@ def test_synthetic_generator_shapes():
     # prefix-consistent: the first 10 test users and the train set are unchanged
     assert np.array_equal(a.tr_len, b.tr_len)
     assert np.array_equal(a.te_len, b.te_len[:10])
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "8"])
+def test_parallel_chunks_identical(tmp_path, monkeypatch, threads):
+    """The multi-threaded reader (chunks cut at line starts, per-thread
+    interning merged afterwards) gives the single-thread corpus; parse errors
+    report the first bad line of the file whichever chunk holds it."""
+    t = synth.config("small")
+    a = t.dataset()
+    paths = [str(tmp_path / n) for n in ("train.txt", "test.txt", "labels.txt")]
+    a.write_tsv(*paths)
+    monkeypatch.setenv("MR_INGEST_MIN_CHUNK", "97")
+    monkeypatch.setenv("MR_INGEST_THREADS", threads)
+    b = Dataset.from_tsv(*paths)
+    for f in ("tr_off", "tr_songs", "te_off", "te_songs", "song_count", "tr_len", "te_len", "lab_off", "lab_songs"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    lines = open(paths[0]).read().splitlines()
+    lines[len(lines) // 2] = "broken"
+    lines[len(lines) - 3] = "also\tbroken"
+    with open(paths[0], "w") as f:
+        f.write("\n".join(lines) + "\n")
+    with pytest.raises(_lib.EngineError) as ei:
+        Dataset.from_tsv(*paths)
+    assert ei.value.code == _lib.MR_E_PARSE and f":{len(lines) // 2 + 1}:" in str(ei.value)
