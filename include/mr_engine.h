@@ -118,7 +118,9 @@ typedef struct mr_options {
                           n_train_users <= 4096, else separate. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
                           to 16384, else 8192); smaller values exercise the chunked path */
-  int32_t reserved[5];
+  int32_t train_order; /* 0 (default) = train users renumbered internally by distinct-song count
+                          (descending) for load balance; 1 = as given. Results are identical. */
+  int32_t reserved[4];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;

@@ -71,7 +71,8 @@ class MrOptions(ctypes.Structure):
         ("time_kernels", c_int32),
         ("stage1", c_int32),
         ("stage1_chunk", c_int32),
-        ("reserved", c_int32 * 5),
+        ("train_order", c_int32),
+        ("reserved", c_int32 * 4),
     ]
 
 

@@ -44,6 +44,8 @@ constexpr int kThreads = 256;             // 4 waves of 64
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxTopK = 64;
 constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS is 160 KiB)
+constexpr int kLdsBytes = 160 * 1024;     // LDS per workgroup (CU) on gfx950
+constexpr int kMaxWideBlockSongs = 65536; // wide shape: uint16 tile-local ids, LDS-bound in practice
 constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64), one chunk
 constexpr int kStage1Chunk = 8192;        // larger train sets: stage 1 in LDS chunks of train users
 constexpr int kMaxChunks = 1024;          // => n_train_users <= 8.4M
@@ -1750,8 +1752,10 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.frac_bits < 8 || o.frac_bits > 40) return fail(MR_E_INVALID, "frac_bits %d outside [8,40]", o.frac_bits);
   if (o.topk < 0 || o.topk > kMaxTopK) return fail(MR_E_INVALID, "topk %d outside [0,%d]", o.topk, kMaxTopK);
   if (o.out_dtype != MR_OUT_F32 && o.out_dtype != MR_OUT_F64) return fail(MR_E_INVALID, "bad out_dtype %d", o.out_dtype);
-  if (o.block_songs < 0 || o.block_songs > kMaxBlockSongs || (o.block_songs % 256) != 0)
-    return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs, kMaxBlockSongs);
+  if (o.block_songs < 0 || o.block_songs > (o.stage1 == 4 ? kMaxWideBlockSongs : kMaxBlockSongs) ||
+      (o.block_songs % 256) != 0)
+    return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs,
+                o.stage1 == 4 ? kMaxWideBlockSongs : kMaxBlockSongs);
   if (o.stage1 < 0 || o.stage1 > 4) return fail(MR_E_INVALID, "stage1 %d outside [0,4]", o.stage1);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
@@ -1841,11 +1845,35 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                   d->song_count[s], col_tr[s] + col_te[s]);
     trs_off[s + 1] = trs_off[s] + col_tr[s];
   }
+  // Train users renumbered by distinct-song count, descending (ties by id),
+  // unless opt.train_order = 1: the users of one wave then have segments of
+  // similar length in every song tile, so no lane waits on one heavy
+  // listener's long tail (heavy listeners dominate every neighbourhood).
+  // Results do not change: every accumulation is an order-free integer sum
+  // and the outputs are indexed by test user and song only.
+  std::vector<int32_t> perm(std::max(1, n_tr));  // new id -> caller's id
+  for (int v = 0; v < n_tr; ++v) perm[v] = v;
+  if (c->opt.train_order == 0)
+    std::stable_sort(perm.begin(), perm.begin() + n_tr, [&](int a, int b) {
+      return d->tr_off[a + 1] - d->tr_off[a] > d->tr_off[b + 1] - d->tr_off[b];
+    });
+  std::vector<int64_t> p_off((size_t)n_tr + 1, 0);
+  std::vector<int32_t> p_songs(std::max<int64_t>(1, d->tr_off[n_tr])), p_len(std::max(1, n_tr));
+  for (int v = 0; v < n_tr; ++v) {
+    const int o = perm[v];
+    const int64_t a = d->tr_off[o], b = d->tr_off[o + 1];
+    std::copy(d->tr_songs + a, d->tr_songs + b, p_songs.begin() + p_off[v]);
+    p_off[v + 1] = p_off[v] + (b - a);
+    p_len[v] = d->tr_len[o];
+  }
+  const int64_t* tr_off = p_off.data();
+  const int32_t* tr_songs = p_songs.data();
+  const int32_t* tr_len = p_len.data();
   std::vector<int32_t> trs_users(std::max<int64_t>(1, trs_off[n_s]));
   {
     std::vector<int64_t> fill(trs_off.begin(), trs_off.end() - 1);
     for (int v = 0; v < n_tr; ++v)
-      for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) trs_users[fill[d->tr_songs[i]]++] = v;
+      for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) trs_users[fill[tr_songs[i]]++] = v;
   }
   // Shard geometry and launch shape.
   const int lo = c->opt.song_lo, hi = c->opt.song_hi > 0 ? c->opt.song_hi : n_s;
@@ -1886,9 +1914,20 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (pull) {
     bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
   } else {
-    bs = c->opt.block_songs > 0 ? c->opt.block_songs
-         : wide               ? (int)std::min<long long>(kMaxBlockSongs, ((long long)width + 255) / 256 * 256)
-                              : auto_block_songs(width, n_te, fused, k, n_tr);
+    if (wide) {
+      // the widest tile the LDS holds (every tile re-walks the user's whole
+      // neighbour list), then balanced: n_tiles = ceil(width / max), bs =
+      // ceil(width / n_tiles) rounded up to 256
+      int bmax = 256;
+      while (bmax + 256 <= 65536 && wide_lds<kWideThreads>(bmax + 256, k, n_chunks).total <= kLdsBytes) bmax += 256;
+      const long long nt = ((long long)width + bmax - 1) / bmax;
+      bs = c->opt.block_songs > 0 ? c->opt.block_songs
+                                  : (int)std::min<long long>(bmax, (((long long)width + nt - 1) / nt + 255) / 256 * 256);
+      if (wide_lds<kWideThreads>(bs, k, n_chunks).total > kLdsBytes)
+        return fail(MR_E_INVALID, "wide shape: block_songs %d needs more than %d B of LDS", bs, kLdsBytes);
+    } else {
+      bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k, n_tr);
+    }
     if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
     if (k > kMaxTopkLarge && bs > kMaxTopkTile)
       return fail(MR_E_INVALID, "with topk > %d block_songs must be <= %d (got %d)", kMaxTopkLarge, kMaxTopkTile, bs);
@@ -1904,7 +1943,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     sqrt_c[s] = std::sqrt((double)d->song_count[s]);
     q_song[s] = (long long)std::nearbyint(two_f / sqrt_c[s]);
   }
-  for (int v = 0; v < n_tr; ++v) sqrt_tr[v] = std::sqrt((double)d->tr_len[v]);
+  for (int v = 0; v < n_tr; ++v) sqrt_tr[v] = std::sqrt((double)tr_len[v]);
   for (int u = 0; u < n_te; ++u) sqrt_te[u] = std::sqrt((double)d->te_len[u]);
   // Tile-major train CSR over the shard's songs: for tile t, user v, the
   // tile-local ids of S(v) ∩ [lo + t*bs, lo + (t+1)*bs) live at
@@ -1913,8 +1952,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const size_t n_tv = pull ? 0 : (size_t)n_tiles * n_tr;
   std::vector<int32_t> toff(n_tv + 1, 0);
   for (int v = 0; v < (pull ? 0 : n_tr); ++v)
-    for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) {
-      const int s = d->tr_songs[i];
+    for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {
+      const int s = tr_songs[i];
       if (s >= lo && s < hi) toff[(size_t)((s - lo) / bs) * n_tr + v + 1]++;
     }
   for (size_t i = 0; i < n_tv; ++i) toff[i + 1] += toff[i];
@@ -1922,8 +1961,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   {
     std::vector<int32_t> fill(toff.begin(), toff.end() - 1);
     for (int v = 0; v < (pull ? 0 : n_tr); ++v)
-      for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) {
-        const int s = d->tr_songs[i];
+      for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {
+        const int s = tr_songs[i];
         if (s < lo || s >= hi) continue;
         const int t = (s - lo) / bs;
         tsongs[fill[(size_t)t * n_tr + v]++] = (uint16_t)(s - lo - t * bs);
@@ -1939,7 +1978,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const int te_stride = (batch + kPullLanes - 1) / kPullLanes * kPullLanes;
 
   hipStream_t st = c->stream;
-  if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(d->tr_off), (size_t)n_tr + 1, st))) return rc;
+  if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(tr_off), (size_t)n_tr + 1, st))) return rc;
   if ((rc = dev_upload(c->te_off, reinterpret_cast<const long long*>(d->te_off), (size_t)n_te + 1, st))) return rc;
   if ((rc = dev_upload(c->te_songs, d->te_songs, (size_t)d->te_off[n_te], st))) return rc;
   if ((rc = dev_upload(c->trs_off, reinterpret_cast<const long long*>(trs_off.data()), trs_off.size(), st))) return rc;
