@@ -1085,6 +1085,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_R
 #define MR_WIDE_R 4         // neighbours per thread per iteration (wide kernel; 2/4/8 within 3%)
 #endif
+#ifndef MR_WIDE_SEG
+#define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
+#endif
 #ifndef MR_WIDE_PREFETCH
 #define MR_WIDE_PREFETCH 0  // 1 = load the next iteration's list entries ahead
 #endif
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
     const int* toff_t = p.toff + (size_t)tile * p.n_tr;
-    constexpr int R = MR_WIDE_R, kSeg = 4;
+    constexpr int R = MR_WIDE_R, kSeg = MR_WIDE_SEG;
     int cur = 0;
     auto load_list = [&](int k0, int (&v)[R], unsigned long long (&q)[R]) {
 #pragma unroll
