@@ -3,7 +3,7 @@ Usage: python scripts/stamps.py [config] [model] [block_songs] [stage1]"""
 import os
 import sys
 
-os.environ["MR_ENGINE_LIB"] = "stamps"
+os.environ.setdefault("MR_ENGINE_LIB", "stamps")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
