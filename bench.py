@@ -222,6 +222,8 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
+    ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "pull", "wide"],
+                    help="launch shape (default: the engine's choice)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -251,7 +253,7 @@ def main() -> None:
         full = synth.config(args.config).dataset()
         lo, hi = n_te * rank // world, n_te * (rank + 1) // world
         blocks = [full.subset_test_users(lo, hi)]
-        engines = [Engine(blocks[0], device=local, out_dtype="f32", topk=10, dense=False)]
+        engines = [Engine(blocks[0], device=local, out_dtype="f32", topk=10, dense=False, stage1=args.stage1)]
         ds = blocks[0]
         eng = engines[0]
         pairs_per_engine = [blocks[0].n_pairs()]
@@ -270,7 +272,7 @@ def main() -> None:
         full = synth.config(args.config, n_test=n_te * nb).dataset()
         blocks = [full.subset_test_users(b * n_te, (b + 1) * n_te)
                   for b in range(rank * args.inflight, (rank + 1) * args.inflight)]
-        engines = [Engine(b, device=local, out_dtype="f32", topk=10) for b in blocks]
+        engines = [Engine(b, device=local, out_dtype="f32", topk=10, stage1=args.stage1) for b in blocks]
         ds = blocks[0]
         eng = engines[0]
         pairs_per_engine = [b.n_pairs() for b in blocks]

@@ -282,14 +282,14 @@ __device__ __forceinline__ void lane_sort(long long (&rk)[M], int (&rs)[M]) {
 // = none): sort each lane's M, then k rounds of "argmax of the lane heads,
 // the winning lane shifts its list". Lane 0 writes out_k/out_s[0..k),
 // missing slots (-1, -1).
-template <int M>
+template <int M, bool SORTED = false>
 __device__ __forceinline__ void wave_topk_regs(long long (&rk)[M], int (&rs)[M], int k, long long* out_k,
                                                int* out_s) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < M; ++j)
     if (rk[j] < 0) { rk[j] = kKeyNone; rs[j] = INT_MAX; }
-  lane_sort<M>(rk, rs);
+  if (!SORTED) lane_sort<M>(rk, rs);  // SORTED: the lane's list is already in order
   int r = 0;
   for (; r < k; ++r) {
     long long bk = rk[0];
@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       const long long key = (long long)acc[i];
       if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
     }
-    wave_topk_regs<kMaxTopkLarge>(tk, ts, k, wk + w * k, ws + w * k);
+    wave_topk_regs<kMaxTopkLarge, true>(tk, ts, k, wk + w * k, ws + w * k);
   }
   __syncthreads();
   if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) 
     if (key > thr) lane_list_insert(tk, ts, k, key, p.song_lo + i, thr);
   }
   if (neg) atomicOr(p.neg, 1u);
-  wave_topk_regs<kMaxTopkLarge>(tk, ts, k, wk + w * k, ws + w * k);
+  wave_topk_regs<kMaxTopkLarge, true>(tk, ts, k, wk + w * k, ws + w * k);
   __syncthreads();
   if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
   __syncthreads();
