@@ -405,12 +405,13 @@ __device__ __forceinline__ void block_topk(int n, int k, Get get, long long* wk,
 // slots (first k used); thr tracks the k-th key (candidates at or below it
 // cannot enter, except equal keys with a lower song id, which the caller
 // excludes by visiting songs in ascending order per lane).
-__device__ __forceinline__ void lane_list_insert(long long (&tk)[kMaxTopkLarge], int (&ts)[kMaxTopkLarge], int k,
-                                                 long long key, int song, long long& thr) {
+template <int KS>
+__device__ __forceinline__ void lane_list_insert(long long (&tk)[KS], int (&ts)[KS], int k, long long key, int song,
+                                                 long long& thr) {
   long long ck = key;
   int cs = song;
 #pragma unroll
-  for (int t = 0; t < kMaxTopkLarge; ++t) {
+  for (int t = 0; t < KS; ++t) {
     const bool b = t < k && cand_before(ck, cs, tk[t], ts[t]);
     const long long ok = tk[t];
     const int os = ts[t];
@@ -421,7 +422,7 @@ __device__ __forceinline__ void lane_list_insert(long long (&tk)[kMaxTopkLarge],
   }
   long long nt = kKeyNone;
 #pragma unroll
-  for (int t = 0; t < kMaxTopkLarge; ++t) nt = (t == k - 1) ? tk[t] : nt;
+  for (int t = 0; t < KS; ++t) nt = (t == k - 1) ? tk[t] : nt;
   thr = nt;
 }
 
@@ -504,6 +505,7 @@ struct NbrParams {
   int* nbr_v;                // [batch][cap]: chunk c's list at c * chunk
   long long* nbr_q;          // [batch][cap]
   int* nbr_cnt;              // [batch][n_chunks]
+  const int* sbound;         // [n_s][n_chunks+1]: first trs_users index of each chunk (n_chunks > 1)
 };
 
 // First index in the sorted trs_users[lo, hi) whose user is >= v.
@@ -525,7 +527,8 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
                                                 const long long* trs_off, const int* trs_users,
                                                 const long long* q_song, long long* s_lo, long long* s_w,
                                                 int* s_pre, int* s_scan, Add add, Mark mark, bool ranged = false,
-                                                int v0 = 0, int v1 = 0) {
+                                                int v0 = 0, int v1 = 0, const int* sbound = nullptr,
+                                                int chunk_idx = 0, int nc1 = 0) {
   const int tid = threadIdx.x;
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
@@ -533,7 +536,11 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
     if (tid < n) {
       const int s2 = te_songs[base + tid];
       long long lo = trs_off[s2], hi = trs_off[s2 + 1];
-      if (ranged) {
+      if (ranged && sbound) {  // precomputed chunk boundaries of L_tr(s2) (mr_load)
+        const int* b = sbound + (size_t)s2 * nc1 + chunk_idx;
+        lo = b[0];
+        hi = b[1];
+      } else if (ranged) {
         lo = lower_bound_user(trs_users, lo, hi, v0);
         hi = lower_bound_user(trs_users, lo, hi, v1);
       }
@@ -582,14 +589,15 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
                                                       const int* trs_users, const long long* q_song,
                                                       long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
                                                       unsigned* heard, int blo, int bhi, bool ranged = false,
-                                                      int v0 = 0, int v1 = 0) {
+                                                      int v0 = 0, int v1 = 0, const int* sbound = nullptr,
+                                                      int chunk_idx = 0, int nc1 = 0) {
   walk_neighbours<MODEL>(
       t0, t1, te_songs, trs_off, trs_users, q_song, s_lo, s_w, s_pre, s_scan,
       [&](int v, unsigned long long w) { atomicAdd(&Y[v - v0], w); },
       [&](int s2) {
         if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
       },
-      ranged, v0, v1);
+      ranged, v0, v1, sbound, chunk_idx, nc1);
 }
 
 // Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
@@ -619,25 +627,44 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
   for (int i = tid; i < cw; i += kThreads) Y[i] = 0ull;
   __syncthreads();
   accumulate_neighbours<MODEL>(Y, p.te_off[u], p.te_off[u + 1], p.te_songs, p.trs_off, p.trs_users, p.q_song,
-                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0, p.n_chunks > 1, cv0, cv1);
+                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0, p.n_chunks > 1, cv0, cv1, p.sbound, c,
+                               p.n_chunks + 1);
 
+  // Compaction, order kept: wave w owns the contiguous quarter [w*q, (w+1)*q)
+  // of the chunk, counts its non-zeros by ballot (rows of 64, conflict-free
+  // LDS reads), one scan of the 4 wave totals, then writes by ballot rank.
   const double two_f = ldexp(1.0, p.frac_bits);
   const double rs_u = p.sqrt_te[u];
   int* out_v = p.nbr_v + (size_t)bu * p.cap + (size_t)c * p.chunk;
   long long* out_q = p.nbr_q + (size_t)bu * p.cap + (size_t)c * p.chunk;
-  int written = 0;
-  for (int i0 = 0; i0 < cw; i0 += kThreads) {
-    const int i = i0 + tid;
-    const unsigned long long y = (i < cw) ? Y[i] : 0ull;
-    const int flag = y != 0ull;
-    int total;
-    const int pos = block_excl_scan(flag, &total, s_scan);
-    if (flag) {
+  const int lane = tid & 63, w = tid >> 6;
+  const int q4 = (cw + kWaves * 64 - 1) / (kWaves * 64) * 64;  // per-wave span, multiple of 64
+  const int wb = min(cw, w * q4), we = min(cw, wb + q4);
+  int nz = 0;
+  for (int i0 = wb; i0 < we; i0 += 64) {
+    const int i = i0 + lane;
+    nz += __popcll(__ballot(i < we && Y[i] != 0ull));
+  }
+  if (lane == 0) s_scan[w] = nz;
+  __syncthreads();
+  int base = 0, written = 0;
+#pragma unroll
+  for (int x = 0; x < kWaves; ++x) {
+    base += x < w ? s_scan[x] : 0;
+    written += s_scan[x];
+  }
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int i0 = wb; i0 < we; i0 += 64) {
+    const int i = i0 + lane;
+    const unsigned long long y = i < we ? Y[i] : 0ull;
+    const unsigned long long m = __ballot(y != 0ull);
+    if (y != 0ull) {
+      const int pos = base + __popcll(m & below);
       const int v = cv0 + i;
-      out_v[written + pos] = v;
-      out_q[written + pos] = neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
+      out_v[pos] = v;
+      out_q[pos] = neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
     }
-    written += total;
+    base += __popcll(m);
   }
   if (tid == 0) p.nbr_cnt[(size_t)bu * p.n_chunks + c] = written;
 }
@@ -1094,7 +1121,9 @@ constexpr int kWideThreads = 1024;
 #define MR_WIDE_PREFETCH 0  // 1 = load the next iteration's list entries ahead
 #endif
 
-template <int MODEL, typename OutT, int NT>
+// KS: register slots of the per-thread lists (10: k = 10 exactly, the
+// default, compiled in; 16: any k <= 16 at run time).
+template <int MODEL, typename OutT, int NT, int KS>
 __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -1211,8 +1240,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
     acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
   }
-  const int k = p.topk;
-  if (k <= 0) return;
+  const int k = KS == 10 ? 10 : p.topk;
+  if (p.topk <= 0) return;
   __syncthreads();
   MR_STAMP(3);
 
@@ -1223,18 +1252,21 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   {
-    long long tk[kMaxTopkLarge];
-    int ts[kMaxTopkLarge];
+    long long tk[KS];
+    int ts[KS];
 #pragma unroll
-    for (int t = 0; t < kMaxTopkLarge; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
+    for (int t = 0; t < KS; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
     long long thr = kKeyNone;
     for (int i = tid; i < bw; i += NT) {
       const long long key = (long long)acc[i];
       if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
     }
-    wave_topk_regs<kMaxTopkLarge, true>(tk, ts, k, wk + w * k, ws + w * k);
+    MR_STAMP(6);
+    wave_topk_regs<KS, true>(tk, ts, k, wk + w * k, ws + w * k);
+    MR_STAMP(7);
   }
   __syncthreads();
+  MR_STAMP(8);
   if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
   __syncthreads();
   MR_STAMP(4);
@@ -1631,6 +1663,7 @@ struct mr_ctx {
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
   DevBuf<int> te_songs, trs_users, toff, nbr_v, nbr_cnt, cand_song, top_song;
   DevBuf<unsigned short> tsongs;
+  DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
   DevBuf<unsigned char> dense;
@@ -1655,7 +1688,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); te_songs.release(); trs_users.release(); toff.release();
+    tsongs.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -1710,8 +1743,14 @@ void pick_kernels(mr_ctx* c) {
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, true> : k_score<MODEL, float, true>;
   else
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
-  if (c->shape == kShapeWide)
-    c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads> : k_score_wide<MODEL, float, kWideThreads>;
+  if (c->shape == kShapeWide) {
+    if (c->opt.topk == 10)
+      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, 10>
+                                   : k_score_wide<MODEL, float, kWideThreads, 10>;
+    else
+      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, kMaxTopkLarge>
+                                   : k_score_wide<MODEL, float, kWideThreads, kMaxTopkLarge>;
+  }
   c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
   c->col_kernel[MODEL] = k_stage1_columns<MODEL>;
   c->pull_kernel[MODEL] = f64 ? k_pull<MODEL, double> : k_pull<MODEL, float>;
@@ -1993,6 +2032,22 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
   if ((rc = dev_upload(c->toff, toff.data(), toff.size(), st))) return rc;
+  if (!fused && !pull && n_chunks > 1) {
+    // Chunk boundaries of every listener list (sorted by train user): the
+    // chunked stage 1 reads its sub-list bounds instead of searching.
+    const int nc1 = n_chunks + 1;
+    std::vector<int32_t> sb((size_t)n_s * nc1);
+    for (int s2 = 0; s2 < n_s; ++s2) {
+      int64_t pos = trs_off[s2];
+      const int64_t end = trs_off[s2 + 1];
+      for (int cc = 0; cc <= n_chunks; ++cc) {
+        const int64_t bound = (int64_t)cc * chunk;
+        while (pos < end && trs_users[pos] < bound) ++pos;
+        sb[(size_t)s2 * nc1 + cc] = (int32_t)pos;
+      }
+    }
+    if ((rc = dev_upload(c->sbound, sb.data(), sb.size(), st))) return rc;
+  }
   if ((rc = dev_upload(c->tsongs, tsongs.data(), tsongs.size(), st))) return rc;
   if (pull) {
     if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
@@ -2114,7 +2169,7 @@ int run_model(mr_ctx* c, int model) {
       if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) return fail(MR_E_STATE, "separate shape without neighbour buffers");
       NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->chunk, c->n_chunks, c->te_off.p, c->te_songs.p,
                    c->trs_off.p, c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
-                   c->nbr_cnt.p};
+                   c->nbr_cnt.p, c->n_chunks > 1 ? c->sbound.p : nullptr};
       for (int y0 = 0; y0 < nb; y0 += 65535) {
         NbrParams q = np;
         q.user0 = user0 + y0;

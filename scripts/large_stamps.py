@@ -38,7 +38,8 @@ span = end.max() - t0
 dur = end - rt[:, 0]
 print(f"{n_tr}/{n_te} {model}: tiles={tiles} WGs={live.sum()} kernel span {span / 1e3:.2f} ms; "
       f"sum(WG time)/256 = {dur.sum() / 256 / 1e3:.2f} ms")
-for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5)):
+for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5),
+                   (" topk scan", 3, 6), (" topk wave", 6, 7), (" topk barrier", 7, 8), (" topk merge", 8, 4)):
     d = rt[:, b] - rt[:, a]
     print(f"  {name:10s} us med {np.median(d):9.1f} p90 {np.percentile(d, 90):9.1f} max {d.max():9.1f} "
           f"sum share {d.sum() / dur.sum():.3f}")
