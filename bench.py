@@ -235,9 +235,18 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # Rehearsal overrides (never set by the driver): MR_BENCH_BACKEND=gloo and
+    # MR_BENCH_DEVICE=0 let several ranks share one GPU to exercise the N > 1
+    # code paths on a one-GPU box. The real runs use RCCL, one GPU per rank.
+    backend = os.environ.get("MR_BENCH_BACKEND", "nccl")
+    if "MR_BENCH_DEVICE" in os.environ:
+        local = int(os.environ["MR_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     if args.config == "c5":
         run_c5(args, world, rank, local)

@@ -62,6 +62,9 @@ def exchange_topk(songs, keys, group=None):
     n_te, k = songs.shape
     g_songs = torch.empty((world * n_te, k), dtype=songs.dtype, device=songs.device)
     g_keys = torch.empty((world * n_te, k), dtype=keys.dtype, device=keys.device)
+    if songs.is_cuda and dist.get_backend(group) != "nccl":  # gloo rehearsal: gather on the host
+        gs, gk = exchange_topk(songs.cpu(), keys.cpu(), group)
+        return gs.to(songs.device), gk.to(keys.device)
     dist.all_gather_into_tensor(g_songs, songs.contiguous(), group=group)
     dist.all_gather_into_tensor(g_keys, keys.contiguous(), group=group)
     return g_songs.view(world, n_te, k), g_keys.view(world, n_te, k)
