@@ -113,8 +113,8 @@ typedef struct mr_options {
                           Yt[train user][test user] slab, the scoring kernel gathers its rows per
                           song; topk <= 16), 4 = wide (large train sets: chunked stage 1, 16k-song
                           tiles scored by 1024-thread workgroups, separate top-k merge launch;
-                          topk <= 16). Auto: pull from 256 test users (n_train_users <= 16384),
-                          else wide when n_train_users > 16384, else fused when
+                          topk <= 16). Auto: wide when n_train_users > 4096 (topk <= 16), else
+                          pull from 256 test users and 1000 train users, else fused when
                           n_train_users <= 4096, else separate. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
                           to 16384, else 8192); smaller values exercise the chunked path */

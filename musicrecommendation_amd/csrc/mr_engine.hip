@@ -1362,7 +1362,8 @@ __global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) 
 constexpr int kPullLanes = 64;   // users per wave
 constexpr int kPullChunk = 32;   // songs per staged output tile
 constexpr int kPullMaxK = 16;    // running top-k slots per lane (registers)
-constexpr int kPullMinUsers = 256;  // auto shape: pull from this many test users
+constexpr int kPullMinUsers = 256;  // auto shape: pull from this many test users ...
+constexpr int kPullMinTrainUsers = 1000;  // ... and this many train users (up to the fused limit)
 
 struct ColParams {
   int n_tr, user0, te_stride, frac_bits;
@@ -1931,8 +1932,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   else if (c->opt.stage1 == 2) shape = kShapeSeparate;
   else if (c->opt.stage1 == 3) shape = kShapePull;
   else if (c->opt.stage1 == 4) shape = kShapeWide;
-  else if (n_te >= kPullMinUsers && k <= kPullMaxK && n_tr <= kMaxLdsTrainUsers) shape = kShapePull;
-  else if (n_tr > kMaxLdsTrainUsers && k <= kMaxTopkLarge) shape = kShapeWide;
+  // auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep.txt): wide
+  // beats separate and pull above 4096 train users; pull wins for many test
+  // users over a small train set; fused for small sets (C2)
+  else if (n_tr > kMaxFusedTrainUsers && k <= kMaxTopkLarge) shape = kShapeWide;
+  else if (n_te >= kPullMinUsers && k <= kPullMaxK && n_tr >= kPullMinTrainUsers) shape = kShapePull;
   else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
   const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide;
   if (wide && k > kMaxTopkLarge)

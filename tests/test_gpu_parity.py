@@ -344,11 +344,11 @@ def test_test_user_blocks_partition():
 @pytest.mark.parametrize("model", MODELS)
 def test_c3_scale_exact_sampled_users(model, stage1):
     """10k train / 1k test (config 3 shape): exact on a sample of test users.
-    auto selects the pull shape here."""
+    auto selects the wide shape here."""
     t = synth.generate(10_000, 1_000, 3, alpha=0.87)
     ds = t.dataset()
     with Engine(ds, out_dtype="f64", topk=10, stage1=stage1) as e:
-        assert e.shape == ("pull" if stage1 == "auto" else "separate")
+        assert e.shape == ("wide" if stage1 == "auto" else "separate")
         e.run(model)
         dense = e.dense()
         songs, _, keys = e.topk()
