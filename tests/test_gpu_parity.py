@@ -411,3 +411,24 @@ def test_train_order_does_not_change_results(stage1):
                 out.append((e.dense(), *e.topk()))
         assert np.array_equal(out[0][0], out[1][0], equal_nan=True)
         assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][3], out[1][3])
+
+
+@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide"])
+def test_degenerate_inputs(stage1):
+    """Edge cases of the reference's inputs, every launch shape, exact vs the
+    oracle: no train users at all (every score 0, MR:159-166 / MR:249-257 sum
+    over nothing), a single song, and a test user who heard every song (no
+    pair at all: top-k empty)."""
+    cases = {
+        "no_train": ([], ["X\ts1\t1", "X\ts2\t1", "Y\ts3\t1"], ["X\ts3\t1"]),
+        "one_song": (["A\ts1\t1"], ["X\ts1\t1"], ["X\ts1\t1"]),
+        "heard_all": (["A\ts1\t1", "A\ts2\t1"], ["X\ts1\t1", "X\ts2\t1", "Y\ts1\t1"], ["Y\ts2\t1"]),
+    }
+    for name, (train, test, labels) in cases.items():
+        ds = dataset_from_lines(train, test, labels)
+        for model in MODELS:
+            got, songs = check_exact(ds, model, k=3, stage1=stage1)
+            if name == "no_train":
+                assert np.nanmax(got) == 0.0
+            if name in ("one_song", "heard_all"):
+                assert (songs[0] == -1).all()  # X heard every song: no candidate
