@@ -222,7 +222,7 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
-    ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "pull", "wide"],
+    ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "pull", "wide", "user"],
                     help="launch shape (default: the engine's choice)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -406,7 +406,8 @@ def main() -> None:
                 "kernel": {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
                            "separate": "k_neighbours + k_score (per step)",
                            "pull": "k_stage1_columns + k_pull + k_topk_merge (per step)",
-                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)"}[eng.shape],
+                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)",
+                           "user": "k_score_user (stages 1+2+3, one workgroup per test user, one launch per step)"}[eng.shape],
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -113,14 +113,20 @@ typedef struct mr_options {
                           Yt[train user][test user] slab, the scoring kernel gathers its rows per
                           song; topk <= 16), 4 = wide (large train sets: chunked stage 1, 16k-song
                           tiles scored by 1024-thread workgroups, separate top-k merge launch;
-                          topk <= 16). Auto: wide when n_train_users > 4096 (topk <= 16), else
-                          pull from 256 test users and 1000 train users, else fused when
-                          n_train_users <= 4096, else separate. */
+                          topk <= 16), 5 = user (one 1024-thread workgroup per test user scores
+                          the whole shard in one LDS tile, stage 1 fused; small catalogues:
+                          shard x 8 B + n_train_users x 8 B within the 160 KiB LDS; topk <= 16).
+                          Auto (topk <= 16): wide when n_train_users > 4096 or n_test_users x
+                          n_train_users >= 1e5, else fused; topk > 16: fused when
+                          n_train_users <= 4096, else separate. Pull and user on request. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
                           to 16384, else 8192); smaller values exercise the chunked path */
   int32_t train_order; /* 0 (default) = train users renumbered internally by distinct-song count
                           (descending) for load balance; 1 = as given. Results are identical. */
-  int32_t reserved[4];
+  int32_t topk_lists;  /* 1 = tile top-k of the wide / user shapes by per-thread running lists only
+                          (diagnostic); 0 (default) = a threshold pass first (about k candidates),
+                          the lists only when ties overflow it. Results are identical. */
+  int32_t reserved[3];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;

@@ -72,7 +72,8 @@ class MrOptions(ctypes.Structure):
         ("stage1", c_int32),
         ("stage1_chunk", c_int32),
         ("train_order", c_int32),
-        ("reserved", c_int32 * 4),
+        ("topk_lists", c_int32),
+        ("reserved", c_int32 * 3),
     ]
 
 

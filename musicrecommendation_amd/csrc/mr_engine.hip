@@ -95,8 +95,10 @@ namespace {
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, stage_lists, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, gm, stage_lists, total;
 };
+// threshold top-k scratch of a 256-thread block (= topk_scratch_bytes<kThreads>())
+constexpr int kTopkScratch256 = (256 / 16 + 1) * 12 + 4 + (256 / 16) * 4 + 256 * 4;
 
 // Separate shape, stage 2: per-wave staging of one round of neighbours
 // (kStgItems segments: start, exclusive prefix of lengths, weight).
@@ -135,6 +137,7 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.flag = o; o = align16(o + 16);
   L.cpre = o; o = align16(o + (n_chunks > 0 ? (n_chunks + 1) * 4 : 0));
   L.stg = o; o = align16(o + (n_chunks > 0 ? kWaves * kStgBytes : 0));
+  L.gm = o; o = align16(o + kTopkScratch256);
   L.total = o;
   return L;
 }
@@ -457,6 +460,134 @@ __device__ __forceinline__ void block_topk_wide(int n, int k, Get get, long long
   __syncthreads();
 }
 
+// Block top-k by threshold, for large n. Candidates are totally ordered by
+// (key desc, song asc) (cand_before), so the k-th best of the NT/16 row bests
+// (16-lane groups) is a lower bound tau on the k-th best entry (those k are k
+// distinct entries): every top-k entry comes before or equal to tau. A second
+// pass collects those entries (about k of them, ties included: the bound is a
+// (key, song) pair) into ck/cs (cap <= 256 slots), and every candidate's rank
+// among them (pairwise comparisons spread over the block) is its output slot.
+// Each thread passes the best of its own keys (mk, ms) — get(i) for
+// i = tid + NT j, which the caller has usually just produced. Scratch gm:
+// topk_scratch_bytes(NT). Returns false, uniformly, when the candidates
+// overflow cap or k > NT/16: the caller then runs the general per-thread-list
+// path. All threads call it; it ends with a barrier. Every phase is spread
+// over the whole block: no single-wave serial chain.
+template <int NT>
+__host__ __device__ constexpr int topk_scratch_bytes() {
+  return (NT / 16 + 1) * 12 + 4 + (NT / 16) * 4 + 256 * 4;
+}
+// The best (key desc, song asc) of a thread's keys get(i), i = tid + NT j.
+static_assert(topk_scratch_bytes<256>() == kTopkScratch256, "score_lds scratch size");
+template <int NT, typename Get>
+__device__ __forceinline__ void thread_best(int n, Get get, long long& mk, int& ms) {
+  mk = kKeyNone;
+  ms = INT_MAX;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < n; i += NT) {
+    long long key;
+    int song;
+    get(i, key, song);
+    if (key >= 0) take_if_before(mk, ms, key, song);
+  }
+}
+template <int NT, typename Get>
+__device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long long mk, int ms, unsigned char* gm,
+                                                     long long* ck, int* cs, int cap, long long* out_k, int* out_s,
+                                                     long long* sb = nullptr) {
+  constexpr int NG = NT / 16;
+  static_assert(NT % 64 == 0 && NG <= 64 && NT >= NG * NG / 4, "block shape");
+  long long* gk = reinterpret_cast<long long*>(gm);    // [NG + 1]: row bests, then tau
+  int* gs = reinterpret_cast<int*>(gk + NG + 1);       // [NG + 1]
+  int* counter = gs + NG + 1;                          // [1]
+  int* grank = counter + 1;                            // [NG]
+  int* crank = grank + NG;                             // [256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (k > NG || k <= 0 || cap > 256) return false;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const long long ok = __shfl_xor(mk, d, 64);
+    const int os = __shfl_xor(ms, d, 64);
+    take_if_before(mk, ms, ok, os);
+  }
+  if ((lane & 15) == 0) { gk[tid >> 4] = mk; gs[tid >> 4] = ms; }
+  if (tid < NG) grank[tid] = 0;
+  if (tid == 0) *counter = 0;
+  __syncthreads();
+  stamp_at(sb, 9);
+  {  // rank of every row best: NG x NG comparisons, NG / (NT / NG) per thread
+    constexpr int SL = NT / NG, PER = (NG + SL - 1) / SL;
+    const int i = tid % NG, j0 = (tid / NG) * PER;
+    const long long mine = gk[i];
+    const int mines = gs[i];
+    int c = 0;
+#pragma unroll
+    for (int jj = 0; jj < PER; ++jj) {
+      const int j = j0 + jj;
+      if (j < NG) {
+        const long long o = gk[j];
+        const int os = gs[j];
+        c += (cand_before(o, os, mine, mines) || (o == mine && os == mines && j < i)) ? 1 : 0;
+      }
+    }
+    if (c) atomicAdd(&grank[i], c);
+  }
+  __syncthreads();
+  if (tid < NG && grank[tid] == k - 1) { gk[NG] = gk[tid]; gs[NG] = gs[tid]; }  // exactly one row
+  if (tid < 256) crank[tid] = 0;
+  __syncthreads();
+  stamp_at(sb, 10);
+  long long tk = gk[NG];
+  int tsg = gs[NG];
+  if (tk < 0) { tk = 0; tsg = INT_MAX; }  // fewer than k valid row bests: every valid key
+#pragma unroll 4
+  for (int i = tid; i < n; i += NT) {
+    long long key;
+    int song;
+    get(i, key, song);
+    if (key >= 0 && !cand_before(tk, tsg, key, song)) {
+      const int pos = atomicAdd(counter, 1);
+      if (pos < cap) { ck[pos] = key; cs[pos] = song; }
+    }
+  }
+  __syncthreads();
+  stamp_at(sb, 11);
+  const int nc = *counter;
+  if (nc > cap) return false;
+  if (nc * nc > 16 * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
+    if (tid < 64) {
+      long long rk[4];
+      int rs[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j;
+        rk[j] = c < nc ? ck[c] : kKeyNone;
+        rs[j] = c < nc ? cs[c] : INT_MAX;
+      }
+      wave_topk_regs<4>(rk, rs, k, out_k, out_s);
+    }
+    __syncthreads();
+    return true;
+  }
+  if (nc > 0) {  // candidate ranks: nc x nc comparisons, <= 16 per thread
+    const int sl = NT / nc;  // slices per candidate (nc <= 256 <= NT)
+    const int per = (nc + sl - 1) / sl;
+    if (tid < sl * nc) {
+      const int i = tid % nc, j0 = (tid / nc) * per;
+      const long long mine = ck[i];
+      const int mines = cs[i];
+      int c = 0;
+      for (int j = j0; j < min(nc, j0 + per); ++j) c += cand_before(ck[j], cs[j], mine, mines) ? 1 : 0;
+      if (c) atomicAdd(&crank[i], c);
+    }
+  }
+  __syncthreads();
+  if (tid < nc && crank[tid] < k) { out_k[crank[tid]] = ck[tid]; out_s[crank[tid]] = cs[tid]; }
+  if (tid >= nc && tid < k) { out_k[tid] = kKeyNone; out_s[tid] = -1; }  // fewer than k entries
+  __syncthreads();
+  return true;
+}
+
 constexpr int kMergeStageBytes = 32 * 1024;  // LDS staging of tile lists per merge pass
 __host__ __device__ inline int merge_lists_per_pass(int k) {
   const int kk = k > 0 ? k : 1;
@@ -707,6 +838,7 @@ struct ScoreParams {
   int* top_song;
   double* top_score;
   long long* stamps;             // diagnostic build: [grid][8] phase timestamps
+  int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -957,7 +1089,16 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     key = (long long)acc[i];
     song = blo + i;
   };
-  if (bs <= kMaxTopkTile) {
+  bool thr_done = false;  // threshold pass first (about k candidates, ranked in parallel)
+  if (!p.topk_lists && k <= kThreads / 16) {
+    long long mk;
+    int ms;
+    thread_best<kThreads>(bw, get_key, mk, ms);
+    thr_done = block_topk_threshold<kThreads>(bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK,
+                                              fk, fs);
+  }
+  if (thr_done) {
+  } else if (bs <= kMaxTopkTile) {
     block_topk(bw, k, get_key, wk, ws, fk, fs);
   } else {
     long long* lk = reinterpret_cast<long long*>(smem_raw + L.acc);
@@ -1038,8 +1179,19 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       }
       __syncthreads();
       MR_STAMP(6);
-      if (w == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
-      __syncthreads();
+      bool merged = false;
+      if (!p.topk_lists && done == 0 && nl == p.n_tiles && k <= kThreads / 16) {  // one pass: threshold select
+        auto get_c = [&](int i, long long& key, int& song) { key = mk[i]; song = ms[i]; };
+        long long bk;
+        int bsg;
+        thread_best<kThreads>(nl * k, get_c, bk, bsg);
+        merged = block_topk_threshold<kThreads>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm, wk, ws,
+                                                kWaves * kMaxTopK, fk, fs);
+      }
+      if (!merged) {
+        if (w == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
+        __syncthreads();
+      }
       MR_STAMP(8);
       done += nl;
       off = 1;
@@ -1090,7 +1242,7 @@ __device__ __forceinline__ int block_excl_scan_nt(int x, int* total, int* sbuf) 
 
 template <int NT>
 struct WideLds {
-  int acc, heard, cpre, s_scan, wk, ws, fk, fs, total;
+  int acc, heard, cpre, s_scan, wk, ws, fk, fs, gm, total;
 };
 template <int NT>
 __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
@@ -1106,6 +1258,7 @@ __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
   L.ws = o; o = align16(o + NW * kk * 4);
   L.fk = o; o = align16(o + kk * 8);
   L.fs = o; o = align16(o + kk * 4);
+  L.gm = o; o = align16(o + topk_scratch_bytes<NT>());
   L.total = o;
   return L;
 }
@@ -1223,7 +1376,15 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 #pragma unroll
         for (int j = 0; j < kSeg; ++j)
           if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q[r]);
-        for (int x = a[r] + kSeg; x < b[r]; ++x) atomicAdd(&acc[p.tsongs[x]], q[r]);
+        // long segments (heavy listeners): kSeg independent loads per batch
+        for (int x0 = a[r] + kSeg; x0 < b[r]; x0 += kSeg) {
+          int st[kSeg];
+#pragma unroll
+          for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b[r] ? (int)p.tsongs[x0 + j] : -1;
+#pragma unroll
+          for (int j = 0; j < kSeg; ++j)
+            if (st[j] >= 0) atomicAdd(&acc[st[j]], q[r]);
+        }
       }
     }
   }
@@ -1251,7 +1412,14 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
   long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
-  {
+  auto get_key = [&](int i, long long& key, int& song) { key = (long long)acc[i]; song = blo + i; };
+  long long mk;
+  int ms;
+  thread_best<NT>(bw, get_key, mk, ms);
+  const bool fast = !p.topk_lists && block_topk_threshold<NT>(bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws,
+                                                              min(256, NW * k), fk, fs);
+  MR_STAMP(6);
+  if (!fast) {  // many ties at the threshold: per-thread running lists
     long long tk[KS];
     int ts[KS];
 #pragma unroll
@@ -1261,14 +1429,13 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       const long long key = (long long)acc[i];
       if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
     }
-    MR_STAMP(6);
     wave_topk_regs<KS, true>(tk, ts, k, wk + w * k, ws + w * k);
-    MR_STAMP(7);
+    __syncthreads();
+    if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
+    __syncthreads();
   }
-  __syncthreads();
+  MR_STAMP(7);
   MR_STAMP(8);
-  if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
-  __syncthreads();
   MR_STAMP(4);
   if (p.n_tiles == 1) {
     for (int r = tid; r < k; r += NT) {
@@ -1286,6 +1453,242 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   }
   MR_STAMP(5);
   (void)lane;
+}
+
+// ---------------------------------------------------------------------------
+// user shape: one 1024-thread workgroup per test user scores the whole shard
+// in one LDS tile, stage 1 included — no neighbour lists in HBM, no tile
+// hand-off, no merge: three dependent gathers (T(u) -> listeners -> their
+// songs) and the top-k, in one launch. For small catalogues (the shard's
+// int64 accumulators + the train users' weights fit the 160 KiB LDS, e.g. the
+// C2 subset: 16770 songs x 500 train users). MR:140-166 / MR:230-257.
+// ---------------------------------------------------------------------------
+constexpr int kUserRound = 512;  // train users staged per stage-2 round
+constexpr int kUserMaxPerThread = 20;  // songs per thread: 20 x 1024 x 8 B = the whole LDS
+// Not chosen automatically: at C2 (10 test users) one workgroup per user
+// leaves 246 CUs idle and its three dependent gathers are latency-bound
+// (31.7 us vs 26.6 us fused); scripts/shape_sweep.py has the other sizes.
+constexpr bool kUserAuto = false;
+template <int NT>
+struct UserLds {
+  int acc, heard, y, st_a, st_pre, st_q, s_scan, wk, ws, fk, fs, gm, total;
+};
+template <int NT>
+__host__ __device__ inline UserLds<NT> user_lds(int bs, int n_tr, int k) {
+  constexpr int NW = NT / 64;
+  const int kk = k > 0 ? k : 1;
+  UserLds<NT> L;
+  int o = 0;
+  const int s1 = NT * 16 + (NT + 1) * 4;  // stage-1 staging (s_lo, s_w, s_pre), aliases acc
+  L.acc = o; o = align16(o + (bs * 8 > s1 ? bs * 8 : s1));
+  L.heard = o; o = align16(o + ((bs + 31) / 32) * 4);
+  L.y = o; o = align16(o + (n_tr > 0 ? n_tr : 1) * 8);
+  L.st_a = o; o = align16(o + kUserRound * 4);
+  L.st_pre = o; o = align16(o + (kUserRound + 1) * 4);
+  L.st_q = o; o = align16(o + kUserRound * 8);
+  L.s_scan = o; o = align16(o + NW * 4);
+  L.wk = o; o = align16(o + NW * kk * 8);
+  L.ws = o; o = align16(o + NW * kk * 4);
+  L.fk = o; o = align16(o + kk * 8);
+  L.fs = o; o = align16(o + kk * 4);
+  L.gm = o; o = align16(o + topk_scratch_bytes<NT>());
+  L.total = o;
+  return L;
+}
+
+template <int MODEL, typename OutT, int KS>
+__global__ __launch_bounds__(kWideThreads) void k_score_user(ScoreParams p) {
+  constexpr int NT = kWideThreads, NW = NT / 64;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const UserLds<NT> L = user_lds<NT>(p.block_songs, p.n_tr, p.topk);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
+  unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
+  unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + L.s_scan);
+  const int bu = blockIdx.x;
+  const int u = p.user0 + bu;
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int blo = p.song_lo, bhi = p.song_hi, bw = bhi - blo;
+  const double two_f = ldexp(1.0, p.frac_bits);
+  MR_STAMP(0);
+  // this thread's epilogue scales (songs tid + NT j), loaded now: they land
+  // while stages 1-2 run
+  double sc[kUserMaxPerThread];
+#pragma unroll
+  for (int j = 0; j < kUserMaxPerThread; ++j) {
+    const int i = tid + j * NT;
+    sc[j] = (MODEL == MR_IBM && i < bw) ? p.sqrt_c[blo + i] : 1.0;
+  }
+
+  for (int i = tid; i < p.n_tr; i += NT) Y[i] = 0ull;
+  for (int i = tid; i < (bw + 31) / 32; i += NT) heard[i] = 0u;
+  __syncthreads();
+
+  // stage 1: Y[v] += w(s2) over v in L_tr(s2), s2 in T(u) (MR:140-149 /
+  // MR:230-239), flattened over NT songs of T(u) at a time.
+  {
+    long long* s_lo = reinterpret_cast<long long*>(smem_raw + L.acc);
+    long long* s_w = s_lo + NT;
+    int* s_pre = reinterpret_cast<int*>(s_w + NT);
+    const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+    for (long long base = t0; base < t1; base += NT) {
+      const int n = (int)min((long long)NT, t1 - base);
+      int len = 0;
+      if (tid < n) {
+        const int s2 = p.te_songs[base + tid];
+        const long long lo = p.trs_off[s2], hi = p.trs_off[s2 + 1];
+        len = (int)(hi - lo);
+        s_lo[tid] = lo;
+        s_w[tid] = MODEL == MR_IBM ? p.q_song[s2] : 1ll;
+        if (s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
+      }
+      int total;
+      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
+      s_pre[tid] = pre;
+      __syncthreads();
+      constexpr int E = 8;
+      for (int i0 = tid; i0 < total; i0 += E * NT) {
+        int v[E];
+        unsigned long long wv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = i0 + e * NT;
+          v[e] = -1;
+          wv[e] = 0ull;
+          if (i < total) {
+            int a = 0, b = n;  // last song j with s_pre[j] <= i
+            while (b - a > 1) {
+              const int m = (a + b) >> 1;
+              if (s_pre[m] <= i) a = m; else b = m;
+            }
+            v[e] = p.trs_users[s_lo[a] + (i - s_pre[a])];
+            wv[e] = (unsigned long long)s_w[a];
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (v[e] >= 0) atomicAdd(&Y[v[e]], wv[e]);
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < bw; i += NT) acc[i] = 0ull;  // the staging above is done
+  __syncthreads();
+  MR_STAMP(1);
+
+  // stage 2: rounds of kUserRound train users; their segment lengths are
+  // scanned so the entries spread evenly over the workgroup (segments are
+  // whole histories here, heavy-tailed).
+  {
+    int* st_a = reinterpret_cast<int*>(smem_raw + L.st_a);
+    int* st_pre = reinterpret_cast<int*>(smem_raw + L.st_pre);
+    unsigned long long* st_q = reinterpret_cast<unsigned long long*>(smem_raw + L.st_q);
+    const double rs_u = p.sqrt_te[u];
+    for (int r0 = 0; r0 < p.n_tr; r0 += kUserRound) {
+      int len = 0;
+      if (tid < kUserRound) {
+        const int v = r0 + tid;
+        int a = 0;
+        if (v < p.n_tr) {
+          const unsigned long long y = Y[v];
+          if (y != 0ull) {
+            a = p.toff[v];
+            len = p.toff[v + 1] - a;
+            st_q[tid] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0,
+                                                                    two_f);
+          }
+        }
+        st_a[tid] = a;
+      }
+      int total;
+      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
+      if (tid < kUserRound) st_pre[tid] = pre;
+      __syncthreads();
+      constexpr int E = 16;
+      for (int j0 = tid; j0 < total; j0 += E * NT) {
+        int song[E], it[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int j = j0 + e * NT;
+          song[e] = -1;
+          it[e] = 0;
+          if (j < total) {
+            int lo = 0, hi = kUserRound;  // last item with st_pre[item] <= j
+#pragma unroll
+            for (int st = 0; st < 9; ++st) {
+              const int m = (lo + hi) >> 1;
+              if (st_pre[m] <= j) lo = m; else hi = m;
+            }
+            song[e] = (int)p.tsongs[st_a[lo] + (j - st_pre[lo])];
+            it[e] = lo;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (song[e] >= 0) atomicAdd(&acc[song[e]], st_q[it[e]]);
+      }
+      __syncthreads();
+    }
+  }
+  MR_STAMP(2);
+
+  // epilogue: scores -> dense row; keys back into acc (scale loads batched)
+  const double inv_f = ldexp(1.0, -p.frac_bits);
+  OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width;
+  long long mk = kKeyNone;  // this thread's best key (the top-k's first pass)
+  int ms = INT_MAX;
+#pragma unroll
+  for (int j = 0; j < kUserMaxPerThread; ++j) {
+    const int i = tid + j * NT;
+    if (i < bw) {
+      const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+      double score = (double)(long long)acc[i] * inv_f;
+      if (MODEL == MR_IBM) score = score / sc[j];
+      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      const long long key = h ? kKeyNone : __double_as_longlong(score);
+      acc[i] = (unsigned long long)key;
+      if (key >= 0) take_if_before(mk, ms, key, blo + i);
+    }
+  }
+  if (p.topk <= 0) return;
+  const int k = KS == 10 ? 10 : p.topk;
+  __syncthreads();
+  MR_STAMP(3);
+
+  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
+  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
+  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
+  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
+  const bool fast = !p.topk_lists && block_topk_threshold<NT>(
+      bw, k, [&](int i, long long& key, int& song) { key = (long long)acc[i]; song = blo + i; }, mk, ms,
+      smem_raw + L.gm, wk, ws, min(256, NW * k), fk, fs
+#ifdef MR_STAMPS
+      , p.stamps ? p.stamps + (size_t)blockIdx.x * kStampSlots : nullptr
+#endif
+      );
+  if (!fast) {  // many ties at the threshold: per-thread running lists
+    long long tk[KS];
+    int ts[KS];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
+    long long thr = kKeyNone;
+    for (int i = tid; i < bw; i += NT) {
+      const long long key = (long long)acc[i];
+      if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
+    }
+    wave_topk_regs<KS, true>(tk, ts, k, wk + w * k, ws + w * k);
+    __syncthreads();
+    if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
+    __syncthreads();
+  }
+  MR_STAMP(4);
+  for (int r = tid; r < k; r += NT) {
+    const size_t o = (size_t)u * k + r;
+    p.top_key[o] = fk[r];
+    p.top_song[o] = fs[r];
+    p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+  }
+  MR_STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -1362,8 +1765,10 @@ __global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) 
 constexpr int kPullLanes = 64;   // users per wave
 constexpr int kPullChunk = 32;   // songs per staged output tile
 constexpr int kPullMaxK = 16;    // running top-k slots per lane (registers)
-constexpr int kPullMinUsers = 256;  // auto shape: pull from this many test users ...
-constexpr int kPullMinTrainUsers = 1000;  // ... and this many train users (up to the fused limit)
+// auto shape: wide from this many (test user x train user) pairs of work
+// (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt: wide wins
+// from 500 x 256 and 2000 x 100, fused below 500 x 128 and 2000 x 32)
+constexpr long long kWideMinUserPairs = 100000;
 
 struct ColParams {
   int n_tr, user0, te_stride, frac_bits;
@@ -1636,7 +2041,7 @@ using ColKernel = void (*)(ColParams);
 using PullKernel = void (*)(PullParams);
 
 // Launch shapes (mr_options.stage1 / mr_launch_info).
-enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2, kShapeWide = 3 };
+enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2, kShapeWide = 3, kShapeUser = 4 };
 
 }  // namespace
 
@@ -1744,6 +2149,13 @@ void pick_kernels(mr_ctx* c) {
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, true> : k_score<MODEL, float, true>;
   else
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
+  if (c->shape == kShapeUser) {
+    if (c->opt.topk == 10)
+      c->score_kernel[MODEL] = f64 ? k_score_user<MODEL, double, 10> : k_score_user<MODEL, float, 10>;
+    else
+      c->score_kernel[MODEL] = f64 ? k_score_user<MODEL, double, kMaxTopkLarge>
+                                   : k_score_user<MODEL, float, kMaxTopkLarge>;
+  }
   if (c->shape == kShapeWide) {
     if (c->opt.topk == 10)
       c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, 10>
@@ -1801,7 +2213,10 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
       (o.block_songs % 256) != 0)
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs,
                 o.stage1 == 4 ? kMaxWideBlockSongs : kMaxBlockSongs);
-  if (o.stage1 < 0 || o.stage1 > 4) return fail(MR_E_INVALID, "stage1 %d outside [0,4]", o.stage1);
+  if (o.stage1 < 0 || o.stage1 > 5) return fail(MR_E_INVALID, "stage1 %d outside [0,5]", o.stage1);
+  if (o.topk_lists != 0 && o.topk_lists != 1) return fail(MR_E_INVALID, "topk_lists %d not 0 or 1", o.topk_lists);
+  if (o.stage1 == 5 && o.block_songs != 0)
+    return fail(MR_E_INVALID, "user shape scores the whole shard in one tile: block_songs must be 0");
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
@@ -1927,18 +2342,31 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   // Shape: many test users -> pull (dense Yt, gathers by song); few users and
   // a small train set -> fused; otherwise separate.
   const int k = c->opt.topk;
+  const bool user_fits = k <= kMaxTopkLarge && n_tr <= kMaxFusedTrainUsers && width <= kMaxWideBlockSongs &&
+                         user_lds<kWideThreads>((width + 255) / 256 * 256, n_tr, k).total <= kLdsBytes;
   int shape;
   if (c->opt.stage1 == 1) shape = kShapeFused;
   else if (c->opt.stage1 == 2) shape = kShapeSeparate;
   else if (c->opt.stage1 == 3) shape = kShapePull;
   else if (c->opt.stage1 == 4) shape = kShapeWide;
-  // auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep.txt): wide
-  // beats separate and pull above 4096 train users; pull wins for many test
-  // users over a small train set; fused for small sets (C2)
+  else if (c->opt.stage1 == 5) shape = kShapeUser;
+  // auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt):
+  // wide beats separate and pull above 4096 train users, and fused from ~1e5
+  // (test user x train user) pairs; fused for small sets (C2)
   else if (n_tr > kMaxFusedTrainUsers && k <= kMaxTopkLarge) shape = kShapeWide;
-  else if (n_te >= kPullMinUsers && k <= kPullMaxK && n_tr >= kPullMinTrainUsers) shape = kShapePull;
+  else if ((long long)n_te * n_tr >= kWideMinUserPairs && k <= kMaxTopkLarge) shape = kShapeWide;
+  else if (user_fits && kUserAuto) shape = kShapeUser;
   else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
-  const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide;
+  const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide,
+             user = shape == kShapeUser;
+  const int user_bs = (width + 255) / 256 * 256;
+  if (user) {
+    if (k > kMaxTopkLarge) return fail(MR_E_INVALID, "user shape keeps topk <= %d (got %d)", kMaxTopkLarge, k);
+    if (user_bs > kMaxWideBlockSongs || user_bs > kUserMaxPerThread * kWideThreads ||
+        user_lds<kWideThreads>(user_bs, n_tr, k).total > kLdsBytes)
+      return fail(MR_E_INVALID, "user shape: %d songs x %d train users need more than %d B of LDS", width, n_tr,
+                  kLdsBytes);
+  }
   if (wide && k > kMaxTopkLarge)
     return fail(MR_E_INVALID, "wide shape keeps topk <= %d (got %d)", kMaxTopkLarge, k);
   if (fused && n_tr > kMaxFusedTrainUsers)
@@ -1961,6 +2389,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   int bs;
   if (pull) {
     bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
+  } else if (user) {
+    bs = user_bs;  // one tile: the whole shard
   } else {
     if (wide) {
       // the widest tile the LDS holds (every tile re-walks the user's whole
@@ -2019,7 +2449,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = n_chunks * chunk;
   const size_t budget = (size_t)8 << 30;
-  const int batch = fused  ? n_te
+  const int batch = (fused || user) ? n_te
                     : pull ? std::min(n_te, pull_batch)
                            : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
                                                                       budget / ((size_t)cap * 12)));
@@ -2057,7 +2487,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
     if ((rc = dev_alloc(c->dbg, 1))) return rc;
     MR_HIP(hipMemsetAsync(c->dbg.p, 0, sizeof(unsigned), st));
-  } else if (!fused) {
+  } else if (!fused && !user) {
     if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
@@ -2083,6 +2513,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
   c->score_lds = pull ? 0 : wide ? c->wide_lds
+                           : user ? (size_t)user_lds<kWideThreads>(bs, n_tr, k).total
                                   : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
@@ -2165,7 +2596,7 @@ int run_model(mr_ctx* c, int model) {
         if (rc) return rc;
       }
       ev = &c->ring[(size_t)c->ring_used * 3];
-      c->ring_has_stage1[c->ring_used] = c->shape != kShapeFused;
+      c->ring_has_stage1[c->ring_used] = c->shape != kShapeFused && c->shape != kShapeUser;
       c->ring_used++;
       MR_HIP(hipEventRecord(ev[0], st));
     }
@@ -2258,8 +2689,12 @@ int run_model(mr_ctx* c, int model) {
       sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
-      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
-                         c->score_lds, st, sp);
+      sp.topk_lists = c->opt.topk_lists;
+      if (c->shape == kShapeUser)  // one workgroup per test user, the whole shard
+        hipLaunchKernelGGL(c->score_kernel[model], dim3(ny), dim3(kWideThreads), c->score_lds, st, sp);
+      else
+        hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
+                           c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
       if (wide && k > 0 && c->n_tiles > 1) {  // per-user top-k over the tiles' candidates
         MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,

@@ -29,7 +29,7 @@ class Engine:
     def __init__(self, dataset: Dataset, *, device: int = 0, frac_bits: int = 32, song_lo: int = 0,
                  song_hi: int = 0, block_songs: int = 0, out_dtype: str = "f32", topk: int = 10,
                  dense: bool = True, time_kernels: bool = False, stage1: str = "auto",
-                 stage1_chunk: int = 0, train_order: str = "auto"):
+                 stage1_chunk: int = 0, train_order: str = "auto", topk_lists: bool = False):
         self._L = _lib.lib()
         opt = _lib.MrOptions()
         _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
@@ -42,9 +42,10 @@ class Engine:
         opt.topk = topk
         opt.dense = 1 if dense else 0
         opt.time_kernels = 1 if time_kernels else 0
-        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4}[stage1]
+        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4, "user": 5}[stage1]
         opt.stage1_chunk = stage1_chunk
         opt.train_order = {"auto": 0, "given": 1}[train_order]
+        opt.topk_lists = 1 if topk_lists else 0
         self.opt = opt
         self.dtype = np.float32 if out_dtype == "f32" else np.float64
         self._h = ctypes.c_void_p()
@@ -65,7 +66,7 @@ class Engine:
         fz, bsz, nt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self._L.mr_launch_info(self._h, ctypes.byref(fz), ctypes.byref(bsz), ctypes.byref(nt)),
                    "mr_launch_info")
-        self.shape = {0: "separate", 1: "fused", 2: "pull", 3: "wide"}[fz.value]
+        self.shape = {0: "separate", 1: "fused", 2: "pull", 3: "wide", 4: "user"}[fz.value]
         self.fused, self.block_songs, self.n_tiles = self.shape == "fused", bsz.value, nt.value
 
     # ---- lifecycle ----------------------------------------------------------

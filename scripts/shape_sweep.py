@@ -7,10 +7,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from musicrecommendation_amd import _lib, synth  # noqa: E402
 from musicrecommendation_amd.engine import Engine  # noqa: E402
 
-for n_tr, n_te in ((500, 256), (2000, 1000), (5000, 1000), (10000, 300), (10000, 1000), (16000, 2000)):
+for n_tr, n_te in ((500, 10), (500, 32), (500, 64), (500, 128), (500, 256), (2000, 10), (2000, 32), (2000, 100), (2000, 1000), (5000, 1000), (10000, 300), (10000, 1000), (16000, 2000)):
     ds = synth.generate_bulk(n_tr, n_te, 3).dataset()
     row = [f"{n_tr:6d}/{n_te:5d} songs {ds.n_songs:6d}"]
-    for shape in ("fused", "separate", "pull", "wide"):
+    for shape in ("fused", "separate", "pull", "wide", "user"):
         try:
             with Engine(ds, topk=10, stage1=shape) as e:
                 e.run("ibm")

@@ -224,6 +224,14 @@ def test_launch_shape_selection():
         assert not e.fused
     with pytest.raises(_lib.EngineError):
         Engine(big, stage1="fused")
+    # auto: wide from 1e5 (test user x train user) pairs, fused below, fused / separate for k > 16
+    c2 = synth.config("c2", n_test=200).dataset()
+    with Engine(c2) as e:
+        assert e.shape == "wide"
+    with Engine(c2.subset_test_users(0, 10)) as e:
+        assert e.shape == "fused"
+    with Engine(c2, topk=17) as e:
+        assert e.shape == "fused"
 
 
 @pytest.mark.parametrize("frac_bits", [16, 24, 40])
@@ -251,7 +259,7 @@ def test_topk_only_mode():
     assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "user"])
 @pytest.mark.parametrize("name", ["c1", "c2"])
 @pytest.mark.parametrize("model", MODELS)
 def test_named_configs_exact(name, model, stage1):
@@ -398,7 +406,7 @@ def test_errors_are_codes_not_aborts():
         assert ei.value.code == _lib.MR_E_STATE
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide", "user"])
 def test_train_order_does_not_change_results(stage1):
     """mr_load renumbers train users by history length (load balance); the
     caller's order gives bit-identical scores and lists."""
@@ -413,7 +421,7 @@ def test_train_order_does_not_change_results(stage1):
         assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][3], out[1][3])
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide", "user"])
 def test_degenerate_inputs(stage1):
     """Edge cases of the reference's inputs, every launch shape, exact vs the
     oracle: no train users at all (every score 0, MR:159-166 / MR:249-257 sum
@@ -432,3 +440,46 @@ def test_degenerate_inputs(stage1):
                 assert np.nanmax(got) == 0.0
             if name in ("one_song", "heard_all"):
                 assert (songs[0] == -1).all()  # X heard every song: no candidate
+
+
+@pytest.mark.parametrize("k", [1, 10, 16])
+@pytest.mark.parametrize("model", MODELS)
+def test_user_shape(model, k):
+    """One workgroup per test user over the whole shard (stage 1 fused, no
+    merge): fixtures, C2 and a song shard of it, f64 and f32; the limits fail loudly."""
+    c2 = synth.config("c2", n_test=13).dataset()
+    for ds in (synth_fixture("tiny")[0], synth_fixture("small")[0], c2):
+        check_exact(ds, model, k=k, stage1="user")
+    check_exact(c2, model, k=k, stage1="user", song_lo=1000, song_hi=9000)
+    with Engine(c2, topk=k, stage1="user") as e:
+        assert e.shape == "user" and e.n_tiles == 1
+        g32 = e.score_dense(model)
+    exp, _, _ = native.fp_model(c2, model, k=1)
+    assert np.array_equal(g32, exp.astype(np.float32), equal_nan=True)
+    with Engine(c2, topk=0, out_dtype="f64", stage1="user") as e:  # dense model only
+        assert np.array_equal(e.score_dense(model), exp, equal_nan=True)
+    with pytest.raises(_lib.EngineError):
+        Engine(c2, stage1="user", topk=17)
+    with pytest.raises(_lib.EngineError):
+        Engine(c2, stage1="user", block_songs=256)
+    big = synth.generate_bulk(3000, 4, 5).dataset()  # > 20k songs: the tile does not fit the LDS
+    with pytest.raises(_lib.EngineError):
+        Engine(big, stage1="user")
+
+
+@pytest.mark.parametrize("stage1", ["wide", "user"])
+@pytest.mark.parametrize("model", MODELS)
+def test_topk_paths_identical(model, stage1):
+    """The threshold top-k and the per-thread-list top-k give the same lists,
+    including heavy ties (one train user's unique songs all score the same)."""
+    tie_train = [f"A\ts{i}\t1" for i in range(600)] + ["B\ts0\t1", "B\tx\t1"]
+    tie = dataset_from_lines(tie_train, ["X\ts0\t1", "Y\tx\t1"], ["X\ts5\t1"])
+    for ds in (synth.config("c2", n_test=13).dataset(), tie):
+        for k in (1, 10, 16):
+            out = []
+            for lists in (False, True):
+                with Engine(ds, out_dtype="f64", topk=k, stage1=stage1, topk_lists=lists) as e:
+                    e.run(model)
+                    out.append(e.topk())
+            assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][2], out[1][2])
+        check_exact(ds, model, k=10, stage1=stage1)
