@@ -160,13 +160,16 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
             maps[name] = ens.threshold_map(t)
         return models
 
+    models = None
     for _ in range(args.warmup):
-        step()
+        models = None  # release the previous step's buffers so the allocator reuses them
+        models = step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        models = None
         models = step()
     torch.cuda.synchronize()
     if world > 1:

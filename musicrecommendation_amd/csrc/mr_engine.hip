@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -97,8 +98,9 @@ namespace {
 struct ScoreLds {
   int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, gm, stage_lists, total;
 };
-// threshold top-k scratch of a 256-thread block (= topk_scratch_bytes<kThreads>())
-constexpr int kTopkScratch256 = (256 / 16 + 1) * 12 + 4 + (256 / 16) * 4 + 256 * 4;
+// threshold top-k scratch of a 256-thread block with up to 64 rows
+// (= topk_scratch_bytes<kThreads, 64>())
+constexpr int kTopkScratch256 = (64 + 1) * 12 + 4 + 64 * 4 + 256 * 4;
 
 // Separate shape, stage 2: per-wave staging of one round of neighbours
 // (kStgItems segments: start, exclusive prefix of lengths, weight).
@@ -473,12 +475,12 @@ __device__ __forceinline__ void block_topk_wide(int n, int k, Get get, long long
 // overflow cap or k > NT/16: the caller then runs the general per-thread-list
 // path. All threads call it; it ends with a barrier. Every phase is spread
 // over the whole block: no single-wave serial chain.
-template <int NT>
+template <int NT, int NG = NT / 16>
 __host__ __device__ constexpr int topk_scratch_bytes() {
-  return (NT / 16 + 1) * 12 + 4 + (NT / 16) * 4 + 256 * 4;
+  return (NG + 1) * 12 + 4 + NG * 4 + 256 * 4;
 }
 // The best (key desc, song asc) of a thread's keys get(i), i = tid + NT j.
-static_assert(topk_scratch_bytes<256>() == kTopkScratch256, "score_lds scratch size");
+static_assert(topk_scratch_bytes<256, 64>() == kTopkScratch256, "score_lds scratch size");
 template <int NT, typename Get>
 __device__ __forceinline__ void thread_best(int n, Get get, long long& mk, int& ms) {
   mk = kKeyNone;
@@ -491,12 +493,15 @@ __device__ __forceinline__ void thread_best(int n, Get get, long long& mk, int& 
     if (key >= 0) take_if_before(mk, ms, key, song);
   }
 }
-template <int NT, typename Get>
+// NG rows of NT / NG threads: more rows give a tighter tau (fewer survivors
+// to rank) for NG^2 / NT comparisons per thread.
+template <int NT, typename Get, int NG = NT / 16>
 __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long long mk, int ms, unsigned char* gm,
                                                      long long* ck, int* cs, int cap, long long* out_k, int* out_s,
                                                      long long* sb = nullptr) {
-  constexpr int NG = NT / 16;
-  static_assert(NT % 64 == 0 && NG <= 64 && NT >= NG * NG / 4, "block shape");
+  constexpr int GS = NT / NG;  // threads per row
+  static_assert(NT % 64 == 0 && NT % NG == 0 && NG <= 64 && GS <= 64 && NT * 16 >= NG * NG,
+                "block shape");
   long long* gk = reinterpret_cast<long long*>(gm);    // [NG + 1]: row bests, then tau
   int* gs = reinterpret_cast<int*>(gk + NG + 1);       // [NG + 1]
   int* counter = gs + NG + 1;                          // [1]
@@ -505,12 +510,12 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   const int tid = threadIdx.x, lane = tid & 63;
   if (k > NG || k <= 0 || cap > 256) return false;
 #pragma unroll
-  for (int d = 1; d < 16; d <<= 1) {
+  for (int d = 1; d < GS; d <<= 1) {
     const long long ok = __shfl_xor(mk, d, 64);
     const int os = __shfl_xor(ms, d, 64);
     take_if_before(mk, ms, ok, os);
   }
-  if ((lane & 15) == 0) { gk[tid >> 4] = mk; gs[tid >> 4] = ms; }
+  if ((lane & (GS - 1)) == 0) { gk[tid / GS] = mk; gs[tid / GS] = ms; }
   if (tid < NG) grank[tid] = 0;
   if (tid == 0) *counter = 0;
   __syncthreads();
@@ -826,6 +831,7 @@ struct ScoreParams {
   int cap;
   int chunk, n_chunks;           // per-chunk neighbour lists (k_neighbours)
   int n_users, xcd_remap;        // users of this launch; 1 = all tiles of a user on one XCD
+  int merge_rows;                // threshold rows of the in-launch merge (16 / 32 / 64; MR_MERGE_ROWS)
   const int* nbr_v;
   const long long* nbr_q;
   const int* nbr_cnt;
@@ -1185,8 +1191,15 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         long long bk;
         int bsg;
         thread_best<kThreads>(nl * k, get_c, bk, bsg);
-        merged = block_topk_threshold<kThreads>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm, wk, ws,
-                                                kWaves * kMaxTopK, fk, fs);
+        if (p.merge_rows == 16)
+          merged = block_topk_threshold<kThreads, decltype(get_c), 16>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
+        else if (p.merge_rows == 64)
+          merged = block_topk_threshold<kThreads, decltype(get_c), 64>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
+        else
+          merged = block_topk_threshold<kThreads, decltype(get_c), 32>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
       }
       if (!merged) {
         if (w == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
@@ -2126,8 +2139,20 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
   return MR_OK;
 }
 
+// Rows of the in-launch merge's threshold pass: 32 (C2 step 20.4 us vs 22.9 at
+// 16 rows and 20.8 at 64, profiles/r01_final/c2_merge_rows.txt);
+// MR_MERGE_ROWS=16/32/64 overrides it for experiments.
+int merge_rows_opt() {
+  static const int rows = [] {
+    const char* e = std::getenv("MR_MERGE_ROWS");
+    const int r = e ? std::atoi(e) : 32;
+    return (r == 16 || r == 64) ? r : 32;
+  }();
+  return rows;
+}
+
 int auto_block_songs(int width, int n_te, bool fused, int k, int n_tr) {
-  // Aim for >= ~1024 workgroups, tiles of 256..16384 songs; with top-k a tile
+  // Separate: aim for >= ~1024 workgroups, tiles of 256..16384 songs; with top-k a tile
   // is at most kMaxTopkTile songs (4 candidates per lane in registers); the
   // fused path keeps the neighbour array beside the tile (<= 8192).
   // Large train sets (chunked stage 1): every tile re-walks the user's whole
@@ -2136,7 +2161,11 @@ int auto_block_songs(int width, int n_te, bool fused, int k, int n_tr) {
   if (!fused && n_tr > kMaxLdsTrainUsers && k <= kMaxTopkLarge)
     return (int)std::max<long long>(256, std::min<long long>(kMaxBlockSongs, cover));
   const long long cap = k > 0 ? kMaxTopkTile : (fused ? 8192 : kMaxBlockSongs);
-  long long want = ((long long)width * std::max(1, n_te) + 1023) / 1024;
+  // Fused: every tile repeats stage 1 and adds a candidate list to the
+  // user's merge, so aim for ~384 workgroups (C2: 33 tiles of 512 songs,
+  // 22.6 us vs 25.5 us at 256, scripts/c2_bs_sweep.py, profiles/r01_final).
+  const long long target = fused ? 384 : 1024;
+  long long want = ((long long)width * std::max(1, n_te) + target - 1) / target;
   long long bs = ((want + 255) / 256) * 256;
   bs = std::max<long long>(256, std::min<long long>(cap, bs));
   return (int)std::max<long long>(256, std::min(bs, cover));
@@ -2672,6 +2701,7 @@ int run_model(mr_ctx* c, int model) {
       ScoreParams sp{};
       sp.chunk = c->chunk; sp.n_chunks = c->n_chunks;
       sp.n_users = ny; sp.xcd_remap = remap;
+      sp.merge_rows = merge_rows_opt();
       sp.n_tr = c->n_tr;
       sp.user0 = user0 + y0;
       sp.song_lo = c->song_lo; sp.song_hi = c->song_hi; sp.width = c->width;

@@ -67,49 +67,84 @@ __host__ __device__ inline float pair_uniform(unsigned long long seed, long long
   return (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
 }
 
+constexpr int kCombPer = 4;  // songs per thread (strided by kThreads: coalesced)
+
+// One (user, kThreads * kCombPer-song block) per workgroup. The pair index
+// needs |{t in T(u): t < s}|: one binary search per block for the first heard
+// song at or after the block, then the few heard songs inside the block are
+// walked per element (T(u) is sorted; rows are short).
 template <typename OutT>
 __global__ __launch_bounds__(kThreads) void k_combine(CombParams p) {
   const int u = blockIdx.y;
-  const int i = blockIdx.x * kThreads + threadIdx.x;
-  if (i >= p.width) return;
-  const size_t o = (size_t)u * p.width + i;
-  const OutT* ubm = reinterpret_cast<const OutT*>(p.ubm);
-  const OutT* ibm = reinterpret_cast<const OutT*>(p.ibm);
-  OutT* out = reinterpret_cast<OutT*>(p.out);
+  const int i0 = blockIdx.x * kThreads * kCombPer + threadIdx.x;
+  const size_t row = (size_t)u * p.width;
+  const OutT* ubm = reinterpret_cast<const OutT*>(p.ubm) + row;
+  const OutT* ibm = reinterpret_cast<const OutT*>(p.ibm) + row;
+  OutT* out = reinterpret_cast<OutT*>(p.out) + row;
+  OutT a4[kCombPer], b4[kCombPer];
+#pragma unroll
+  for (int r = 0; r < kCombPer; ++r) {
+    const int i = i0 + r * kThreads;
+    a4[r] = i < p.width ? ubm[i] : (OutT)0;
+    b4[r] = i < p.width ? ibm[i] : (OutT)0;
+  }
   if (p.kind == MR_COMB_LINEAR) {  // MR:327: rank1 * alpha + rank2 * (1 - alpha); NaN stays NaN
-    out[o] = (OutT)((double)ubm[o] * p.param + (double)ibm[o] * (1.0 - p.param));
+#pragma unroll
+    for (int r = 0; r < kCombPer; ++r) {
+      const int i = i0 + r * kThreads;
+      if (i < p.width) out[i] = (OutT)((double)a4[r] * p.param + (double)b4[r] * (1.0 - p.param));
+    }
     return;
   }
-  const int s = p.song_lo + i;
   const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
-  long long a = t0, b = t1;  // first song of T(u) >= s
+  const int s_blk = p.song_lo + blockIdx.x * kThreads * kCombPer;  // first song of the block
+  long long a = t0, b = t1;  // first song of T(u) >= s_blk (uniform over the block)
   while (a < b) {
     const long long m = (a + b) >> 1;
-    if (p.te_songs[m] < s) a = m + 1; else b = m;
+    if (p.te_songs[m] < s_blk) a = m + 1; else b = m;
   }
-  if (a < t1 && p.te_songs[a] == s) {  // heard: no pair (MR:109)
-    out[o] = (OutT)NAN;
-    return;
+#pragma unroll
+  for (int r = 0; r < kCombPer; ++r) {
+    const int i = i0 + r * kThreads;
+    if (i >= p.width) continue;
+    const int s = p.song_lo + i;
+    long long j = a;  // first song of T(u) >= s
+    while (j < t1 && p.te_songs[j] < s) ++j;
+    if (j < t1 && p.te_songs[j] == s) {  // heard: no pair (MR:109)
+      out[i] = (OutT)NAN;
+      continue;
+    }
+    const long long idx = p.pair_base + (long long)u * p.n_songs - t0 + s - (j - t0);
+    const bool take_ibm = p.kind == MR_COMB_AGGREGATION ? idx < p.threshold                   // MR:380-381
+                                                        : (double)pair_uniform(p.seed, idx) < p.param;  // MR:414-415
+    out[i] = take_ibm ? b4[r] : a4[r];
   }
-  const long long idx = p.pair_base + (long long)u * p.n_songs - t0 + s - (a - t0);
-  const bool take_ibm = p.kind == MR_COMB_AGGREGATION ? idx < p.threshold                   // MR:380-381
-                                                      : (double)pair_uniform(p.seed, idx) < p.param;  // MR:414-415
-  out[o] = take_ibm ? ibm[o] : ubm[o];
 }
 
 // ---- evaluation ------------------------------------------------------------
+constexpr int kMinmaxPer = 8;  // loads in flight per thread per iteration
+
 template <typename OutT>
 __global__ __launch_bounds__(kThreads) void k_minmax(const OutT* d, long long n, double* part) {
   __shared__ double smn[kThreads], smx[kThreads];
-  double mn = INFINITY, mx = -INFINITY;
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const double x = (double)d[i];
-    if (x != x) continue;
-    mn = fmin(mn, x);
-    mx = fmax(mx, x);
+  OutT mn = (OutT)INFINITY, mx = (OutT)-INFINITY;  // min/max are exact in the element type
+  const long long stride = (long long)gridDim.x * kThreads;
+  for (long long i0 = (long long)blockIdx.x * kThreads + threadIdx.x; i0 < n; i0 += stride * kMinmaxPer) {
+    OutT x[kMinmaxPer];
+#pragma unroll
+    for (int r = 0; r < kMinmaxPer; ++r) {
+      const long long i = i0 + r * stride;
+      x[r] = i < n ? d[i] : (OutT)NAN;
+    }
+#pragma unroll
+    for (int r = 0; r < kMinmaxPer; ++r) {
+      if (x[r] != x[r]) continue;
+      mn = x[r] < mn ? x[r] : mn;
+      mx = x[r] > mx ? x[r] : mx;
+    }
   }
-  smn[threadIdx.x] = mn;
-  smx[threadIdx.x] = mx;
+  smn[threadIdx.x] = (double)mn;
+  smx[threadIdx.x] = (double)mx;
   __syncthreads();
   for (int h = kThreads / 2; h > 0; h >>= 1) {
     if ((int)threadIdx.x < h) {
@@ -153,12 +188,19 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   int cnt[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) cnt[t] = 0;
-  for (int u = u0; u < u1; ++u) {
-    const double x = (double)d[(size_t)u * p.width + i];
-    if (x != x) continue;
-    const int c = levels(x, p.mn, p.mx);
+  constexpr int U = 8;  // rows in flight per thread
+  for (int ub = u0; ub < u1; ub += U) {
+    OutT x[U];
 #pragma unroll
-    for (int t = 0; t < kThresholds; ++t) cnt[t] += t < c ? 1 : 0;
+    for (int r = 0; r < U; ++r) x[r] = ub + r < u1 ? d[(size_t)(ub + r) * p.width + i] : (OutT)NAN;
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      const double xv = (double)x[r];
+      if (xv != xv) continue;
+      const int c = levels(xv, p.mn, p.mx);
+#pragma unroll
+      for (int t = 0; t < kThresholds; ++t) cnt[t] += t < c ? 1 : 0;
+    }
   }
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t)
@@ -215,7 +257,7 @@ int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_
     q.ubm = (const char*)ubm + (size_t)y0 * width * esz;
     q.ibm = (const char*)ibm + (size_t)y0 * width * esz;
     q.out = (char*)out + (size_t)y0 * width * esz;
-    dim3 grid((width + kThreads - 1) / kThreads, ny);
+    dim3 grid((width + kThreads * kCombPer - 1) / (kThreads * kCombPer), ny);
     if (v.out_dtype == MR_OUT_F64) hipLaunchKernelGGL(k_combine<double>, grid, dim3(kThreads), 0, st, q);
     else hipLaunchKernelGGL(k_combine<float>, grid, dim3(kThreads), 0, st, q);
     MR_HIP(hipGetLastError());
@@ -231,7 +273,7 @@ int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx
   if (rc) return rc;
   MR_HIP(hipSetDevice(v.device));
   const long long n = (long long)v.n_test_users * (v.song_hi - v.song_lo);
-  const int blocks = (int)std::max<long long>(1, std::min<long long>(1024, (n + kThreads - 1) / kThreads));
+  const int blocks = (int)std::max<long long>(1, std::min<long long>(4096, (n + kThreads - 1) / kThreads));
   Tmp<double> part;
   MR_HIP(hipMalloc(reinterpret_cast<void**>(&part.p), (size_t)blocks * 2 * sizeof(double)));
   hipStream_t st = (hipStream_t)v.stream;
@@ -283,7 +325,7 @@ int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, 
   MR_HIP(hipMemcpyAsync(d_ls.p, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, st));
   // enough (song block x user block) workgroups to fill the chip
   const int sx = (width + kThreads - 1) / kThreads;
-  const int uy = std::max(1, std::min(n_te, (2048 + sx - 1) / sx));
+  const int uy = std::max(1, std::min((n_te + 31) / 32, (8192 + sx - 1) / sx));
   EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
                 n_lab};
   const bool f64 = v.out_dtype == MR_OUT_F64;

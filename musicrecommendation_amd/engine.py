@@ -162,12 +162,17 @@ class Engine:
         return mn.value, mx.value
 
     def eval_counts(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray,
-                    lab_songs: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-        """(pred, tp) counts, each width x 10 int32 (MR:529, MR:541-553)."""
+                    lab_songs: np.ndarray, pred: Optional[np.ndarray] = None,
+                    tp: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """(pred, tp) counts, each width x 10 int32 (MR:529, MR:541-553); pred / tp
+        may be caller-owned (e.g. pinned) C-contiguous int32 width x 10 arrays."""
         lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
         lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
-        pred = np.empty((self.width, 10), dtype=np.int32)
-        tp = np.empty((self.width, 10), dtype=np.int32)
+        for a in (pred, tp):
+            if a is not None and (a.dtype != np.int32 or a.shape != (self.width, 10) or not a.flags.c_contiguous):
+                raise ValueError("pred / tp must be C-contiguous int32 arrays of shape (width, 10)")
+        pred = np.empty((self.width, 10), dtype=np.int32) if pred is None else pred
+        tp = np.empty((self.width, 10), dtype=np.int32) if tp is None else tp
         _lib.check(self._L.mr_eval_counts_device(
             self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
             lab_songs.ctypes.data_as(ctypes.c_void_p), pred.ctypes.data_as(ctypes.c_void_p),

@@ -75,6 +75,7 @@ class DeviceEnsemble:
         self.pos = evaluation.label_pos(self.ds) if pos is None else np.asarray(pos, dtype=np.int32)
         self.n_label_songs = int(self.ds.n_label_songs if n_label_songs is None else n_label_songs)
         self.group = group
+        self._host = None  # pinned (pred, tp) count buffers of threshold_map
 
     def empty(self):
         import torch
@@ -133,11 +134,18 @@ class DeviceEnsemble:
             mn, mx = float(a.item()), float(b.item())
         if not (mn <= mx):
             raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
-        pred, tp = self.e.eval_counts(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs)
-        full_p = np.zeros((self.ds.n_songs, 10), dtype=np.int32)
-        full_t = np.zeros_like(full_p)
-        full_p[self.e.song_lo:self.e.song_hi] = pred
-        full_t[self.e.song_lo:self.e.song_hi] = tp
+        if self._host is None and torch.cuda.is_available():  # pinned, reused: no page faults per call
+            self._host = [torch.empty((self.e.width, 10), dtype=torch.int32, pin_memory=True).numpy()
+                          for _ in range(2)]
+        bufs = {} if self._host is None else {"pred": self._host[0], "tp": self._host[1]}
+        pred, tp = self.e.eval_counts(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, **bufs)
+        if self.e.song_lo == 0 and self.e.song_hi == self.ds.n_songs:
+            full_p, full_t = pred, tp
+        else:
+            full_p = np.zeros((self.ds.n_songs, 10), dtype=np.int32)
+            full_t = np.zeros_like(full_p)
+            full_p[self.e.song_lo:self.e.song_hi] = pred
+            full_t[self.e.song_lo:self.e.song_hi] = tp
         if world > 1:
             be = dist.get_backend(self.group)
             dev = self.device if be == "nccl" else torch.device("cpu")

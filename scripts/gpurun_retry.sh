@@ -4,7 +4,7 @@
 # Usage: scripts/gpurun_retry.sh TIMEOUT 'command'
 T=$1; shift
 for i in 1 2 3 4 5 6; do
-  rm -f gpurun_out/*.log
+  rm -f gpurun_out/.last_call.json
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
   rc=$?
   [ $rc -ne 3 ] && exit $rc
