@@ -39,7 +39,9 @@ using mr_host::fail;
 
 constexpr int kThreads = 256;
 constexpr int kThresholds = 10;  // 0.0, 0.1, ..., 0.9 (MR:590)
-__constant__ double kThr[kThresholds] = {0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9};
+#define MR_THRESHOLDS {0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9}
+__constant__ double kThr[kThresholds] = MR_THRESHOLDS;
+constexpr double kThrHost[kThresholds] = MR_THRESHOLDS;
 
 // ---- combination models -----------------------------------------------------
 struct CombParams {
@@ -168,7 +170,31 @@ struct EvalParams {
   const int* lab_u;
   const int* lab_s;
   long long n_lab;
+  float xt_f[kThresholds];   // smallest score with (x - min) / (max - min) > t_i (f32 models)
+  double xt_d[kThresholds];  // the same for f64 models
 };
+
+// The level test (x - mn) / (mx - mn) > t of MR:529 is monotone in x (fp64
+// subtraction and division by a positive range are monotone under rounding),
+// so it equals x >= xt with xt the smallest score of the model's element type
+// that passes. Found on the host by bisection over the ordered bit patterns of
+// that type, with the same fp64 expression: exact, and the kernel then needs
+// 10 compares per element instead of an fp64 division.
+template <typename T, typename U>
+T level_floor(double mn, double mx, double t) {
+  constexpr int B = sizeof(T) * 8;
+  const U sign = (U)1 << (B - 1);
+  auto key = [&](T x) { U b; std::memcpy(&b, &x, sizeof b); return (b & sign) ? (U)~b : (U)(b | sign); };
+  auto val = [&](U k) { U b = (k & sign) ? (U)(k & ~sign) : (U)~k; T x; std::memcpy(&x, &b, sizeof x); return x; };
+  auto pass = [&](U k) { return ((double)val(k) - mn) / (mx - mn) > t; };
+  U lo = key(-INFINITY), hi = key(INFINITY);  // NaN patterns lie outside [lo, hi]
+  if (!pass(hi)) return (T)NAN;               // nothing passes (mx == mn: 0 / 0)
+  while (lo < hi) {                           // smallest passing key
+    const U m = lo + (hi - lo) / 2;
+    if (pass(m)) hi = m; else lo = m + 1;
+  }
+  return val(lo);
+}
 
 __device__ __forceinline__ int levels(double x, double mn, double mx) {
   const double v = (x - mn) / (mx - mn);  // MR:529 (NaN > t is false)
@@ -185,6 +211,9 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   if (i >= p.width) return;
   const int u0 = blockIdx.y * p.users_per_block, u1 = min(p.n_te, u0 + p.users_per_block);
   const OutT* d = reinterpret_cast<const OutT*>(p.dense);
+  OutT xt[kThresholds];
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t) xt[t] = sizeof(OutT) == 4 ? (OutT)p.xt_f[t] : (OutT)p.xt_d[t];
   int cnt[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) cnt[t] = 0;
@@ -194,13 +223,9 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
 #pragma unroll
     for (int r = 0; r < U; ++r) x[r] = ub + r < u1 ? d[(size_t)(ub + r) * p.width + i] : (OutT)NAN;
 #pragma unroll
-    for (int r = 0; r < U; ++r) {
-      const double xv = (double)x[r];
-      if (xv != xv) continue;
-      const int c = levels(xv, p.mn, p.mx);
+    for (int r = 0; r < U; ++r)
 #pragma unroll
-      for (int t = 0; t < kThresholds; ++t) cnt[t] += t < c ? 1 : 0;
-    }
+      for (int t = 0; t < kThresholds; ++t) cnt[t] += x[r] >= xt[t] ? 1 : 0;  // NaN (no pair): never
   }
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t)
@@ -329,6 +354,11 @@ int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, 
   EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
                 n_lab};
   const bool f64 = v.out_dtype == MR_OUT_F64;
+  for (int t = 0; t < kThresholds; ++t) {
+    const double thr = kThrHost[t];
+    ep.xt_f[t] = level_floor<float, uint32_t>(mn, mx, thr);
+    ep.xt_d[t] = level_floor<double, uint64_t>(mn, mx, thr);
+  }
   if (width > 0) {
     if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
     else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
