@@ -56,3 +56,8 @@ end = np.where(last, rt[:, 9], rt[:, 5])
 print("WG end offsets (us) min/med/max", *np.round(np.percentile(end - t0, [0, 50, 100]), 2))
 lu = np.where(last)[0]
 print("last-WG merge start (us) per user:", np.round(rt[lu, 5] - t0, 2).tolist())
+if e.fused and e.shape == "fused":
+    nt = e.n_tiles
+    for name, a, b in (("stage1", 0, 1), ("stage2", 1, 2), ("start", None, 0)):
+        d = (rt[:, b] - (rt[:, a] if a is not None else t0)).reshape(-1, nt)
+        print(f"per-user {name:6s} med/max us:", [(round(float(np.median(r)), 2), round(float(r.max()), 2)) for r in d])
