@@ -692,22 +692,40 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
     __syncthreads();
     // 16 flattened entries per thread in flight: the listener loads of one
     // batch are issued together, then their accumulations.
+    // Segment search (j with s_pre[j] <= i < s_pre[j+1]): groups of 4
+    // entries advance in lockstep for ceil(log2 n) halvings (their LDS reads
+    // overlap); groups past the block's last entry are skipped uniformly.
+    // (A per-entry loop serialised entries x log2 n dependent LDS reads: 7.3 us
+    // of stage 1 for C2's heaviest user; 16-wide lockstep with fixed 8 steps
+    // cost more than it saved.)
+    const int nsteps = n > 1 ? 32 - __clz(n - 1) : 0;
     for (int i0 = tid; i0 < total; i0 += 16 * kThreads) {
+      const int ib = i0 - tid;  // block-uniform
       int v[16];
       unsigned long long wv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = i0 + r * kThreads;
-        v[r] = -1;
-        wv[r] = 0ull;
-        if (i < total) {
-          int a = 0, b = n;  // j with s_pre[j] <= i < s_pre[j+1]
-          while (b - a > 1) {
-            const int m = (a + b) >> 1;
-            if (s_pre[m] <= i) a = m; else b = m;
+      for (int r = 0; r < 16; ++r) { v[r] = -1; wv[r] = 0ull; }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (ib + g * 4 * kThreads >= total) break;
+        int a[4], b[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { a[e] = 0; b[e] = n; }
+        for (int st = 0; st < nsteps; ++st) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = i0 + (g * 4 + e) * kThreads;
+            const int m = (a[e] + b[e]) >> 1;
+            if (s_pre[m] <= i) a[e] = m; else b[e] = m;  // size 1: m = a, stays
           }
-          v[r] = trs_users[s_lo[a] + (i - s_pre[a])];
-          wv[r] = (unsigned long long)s_w[a];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = i0 + (g * 4 + e) * kThreads;
+          if (i < total) {
+            v[g * 4 + e] = trs_users[s_lo[a[e]] + (i - s_pre[a[e]])];
+            wv[g * 4 + e] = (unsigned long long)s_w[a[e]];
+          }
         }
       }
 #pragma unroll
@@ -916,7 +934,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     // 4 neighbours per thread in flight: row-pointer loads, then the first
     // song of each segment, then the LDS atomics.
     for (int v0 = tid; v0 < p.n_tr; v0 += 4 * kThreads) {
-      int a[4], b[4], s0[4];
+      int a[4], b[4];
       unsigned long long y[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -934,16 +952,32 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
           }
         }
       }
+      // the first 4 songs of each of the 4 segments in one batch (16 loads in
+      // flight), then the atomics; longer segments continue 4 at a time
+      // (a song-at-a-time loop left heavy listeners' segments serialised on
+      // load latency).
+      int sg[4][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s0[r] = a[r] < b[r] ? (int)p.tsongs[a[r]] : -1;
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sg[r][e] = a[r] + e < b[r] ? (int)p.tsongs[a[r] + e] : -1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (s0[r] < 0) continue;
+        if (sg[r][0] < 0) continue;
         const int v = v0 + r * kThreads;
         const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
             y[r], rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
-        atomicAdd(&acc[s0[r]], q);
-        for (int x = a[r] + 1; x < b[r]; ++x) atomicAdd(&acc[p.tsongs[x]], q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (sg[r][e] >= 0) atomicAdd(&acc[sg[r][e]], q);
+        for (int x = a[r] + 4; x < b[r]; x += 4) {
+          int t4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t4[e] = x + e < b[r] ? (int)p.tsongs[x + e] : -1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (t4[e] >= 0) atomicAdd(&acc[t4[e]], q);
+        }
       }
     }
   } else {
