@@ -1442,15 +1442,40 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   __syncthreads();
   MR_STAMP(2);
 
-  // epilogue: scores -> dense row segment; keys back into acc
+  // epilogue: scores -> dense row segment; keys back into acc. 8 songs per
+  // thread per batch (the per-song scale loads in flight together), and the
+  // thread's best key (thread_best order: i = tid + NT j) tracked on the way
+  // for the threshold top-k.
   const double inv_f = ldexp(1.0, -p.frac_bits);
   OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
-  for (int i = tid; i < bw; i += NT) {
-    const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
-    double score = (double)(long long)acc[i] * inv_f;
-    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
-    if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
-    acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
+  long long mk = kKeyNone;
+  int ms = INT_MAX;
+  constexpr int EB = 8;
+  for (int i0 = tid; i0 < bw; i0 += EB * NT) {
+    double sc[EB];
+    unsigned long long av[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int i = i0 + e * NT;
+      sc[e] = 1.0;
+      av[e] = 0ull;
+      if (i < bw) {
+        av[e] = acc[i];
+        if (MODEL == MR_IBM) sc[e] = p.sqrt_c[blo + i];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int i = i0 + e * NT;
+      if (i >= bw) continue;
+      const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+      double score = (double)(long long)av[e] * inv_f;
+      if (MODEL == MR_IBM) score = score / sc[e];
+      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      const long long key = h ? kKeyNone : __double_as_longlong(score);
+      acc[i] = (unsigned long long)key;
+      if (key >= 0) take_if_before(mk, ms, key, blo + i);
+    }
   }
   const int k = KS == 10 ? 10 : p.topk;
   if (p.topk <= 0) return;
@@ -1464,9 +1489,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   auto get_key = [&](int i, long long& key, int& song) { key = (long long)acc[i]; song = blo + i; };
-  long long mk;
-  int ms;
-  thread_best<NT>(bw, get_key, mk, ms);
+  // (mk, ms): this thread's best key, from the epilogue
   const bool fast = !p.topk_lists && block_topk_threshold<NT>(bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws,
                                                               min(256, NW * k), fk, fs);
   MR_STAMP(6);
