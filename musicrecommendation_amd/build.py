@@ -31,10 +31,10 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _stale() -> bool:
-    if not os.path.exists(OUT):
+def _stale(out: str = OUT) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     return any(os.path.getmtime(p) > t for p in deps)
 
@@ -43,23 +43,31 @@ OUT_STAMPS = os.path.join(HERE, "libmr_engine_stamps.so")
 OUT_CHECKS = os.path.join(HERE, "libmr_engine_checks.so")
 
 
-def _compile(out: str, extra, verbose: bool) -> None:
+def _compile_all(jobs, verbose: bool) -> None:
+    """Compile the (out, extra flags) variants in parallel (one hipcc each)."""
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, *FLAGS, *extra, f"-I{INCLUDE}", *sources(), "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    procs = []
+    for out, extra in jobs:
+        cmd = [hipcc, *FLAGS, *extra, f"-I{INCLUDE}", *sources(), "-o", out + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((out, cmd, subprocess.Popen(cmd)))
+    failed = [cmd for out, cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    for out, _cmd, _p in procs:
+        os.replace(out + ".tmp", out)
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = True) -> str:
     """Production library; plus the diagnostic variants (phase timestamps,
     bounds-checked pull kernels)."""
-    if force or _stale():
-        _compile(OUT, [], verbose)
-        if stamps:
-            _compile(OUT_STAMPS, ["-DMR_STAMPS"], verbose)
-            _compile(OUT_CHECKS, ["-DMR_CHECKS"], verbose)
+    jobs = [(OUT, [])]
+    if stamps:
+        jobs += [(OUT_STAMPS, ["-DMR_STAMPS"]), (OUT_CHECKS, ["-DMR_CHECKS"])]
+    jobs = [(o, x) for o, x in jobs if force or _stale(o)]
+    if jobs:
+        _compile_all(jobs, verbose)
     return OUT
 
 

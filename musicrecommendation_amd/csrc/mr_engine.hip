@@ -1162,6 +1162,16 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   }
 
   // Publish the tile's candidates (sc1), then count the tile in.
+  // Ordering: this is the measured valid hand-off of MI355X_MICROARCH.md
+  // ("Hand-offs measured with sc1 loads in place of the acquire", row 1):
+  // every byte stored sc1 (write-through, dropped from L1/L2), every storing
+  // wave waits vmcnt(0) (inline asm with a memory clobber, so the compiler
+  // cannot sink a store below it), a workgroup barrier, ONE lane's agent-scope
+  // atomic add; the last adder's workgroup reads only after a barrier it
+  // joins, with sc1 loads (L1 bypassed). A release/acquire fence pair at agent
+  // scope would lower to buffer_wbl2 sc1 + buffer_inv sc1 — a write-back of
+  // the XCD's whole L2 (≈1.7-6.5 us per the guide's price table) on every
+  // tile's critical path — and adds nothing this protocol needs on gfx950.
   long long* ck = p.cand_key + (size_t)u * p.n_tiles * k;
   int* cs = p.cand_song + (size_t)u * p.n_tiles * k;
   for (int r = tid; r < k; r += kThreads) {

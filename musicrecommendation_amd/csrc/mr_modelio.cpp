@@ -35,10 +35,33 @@ using mr_host::fail;
 // and the decimal exponent e of the first digit (x = d.ddd x 10^e). The JDK 19
 // rule: among the decimals of minimal length m that read back to x, the one
 // closest to x; when m = 1, the closest among lengths 1 and 2 (so
-// Double.MIN_VALUE is 4.9E-324, not 5.0E-324). A correctly rounded p-digit
-// decimal is the closest p-digit one, and every 1-digit decimal is a 2-digit one.
+// Double.MIN_VALUE is 4.9E-324, not 5.0E-324). At each length p the
+// correctly rounded p-digit decimal is the closest one; when it does not read
+// back (the rounding interval of a power of two is asymmetric, e.g. 2^-24), its
+// p-digit neighbours one unit in the last digit away still may: they are
+// tried before moving on to p + 1 digits (the closest one that reads back wins).
+namespace {
+bool reads_back(unsigned long long m, int exp10, double x, long double* dist) {
+  char b[48];
+  std::snprintf(b, sizeof b, "%llue%d", m, exp10);
+  const double y = std::strtod(b, nullptr);
+  if (y != std::fabs(x)) return false;
+  *dist = std::fabs(std::strtold(b, nullptr) - (long double)std::fabs(x));
+  return true;
+}
+}  // namespace
+
 void shortest_digits(double x, std::string& digits, int& e) {
   char buf[64];
+  auto take = [&](const char* str) {
+    const char* s = str;
+    if (*s == '-') ++s;
+    digits.clear();
+    for (; *s && *s != 'e'; ++s)
+      if (*s >= '0' && *s <= '9') digits.push_back(*s);
+    e = std::atoi(s + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  };
   for (int p = 1; p <= 17; ++p) {
     std::snprintf(buf, sizeof buf, "%.*e", p - 1, x);  // correctly rounded to p digits
     if (std::strtod(buf, nullptr) == x || p == 17) {
@@ -47,12 +70,27 @@ void shortest_digits(double x, std::string& digits, int& e) {
         std::snprintf(b2, sizeof b2, "%.1e", x);
         if (std::strtod(b2, nullptr) == x) std::memcpy(buf, b2, sizeof b2);
       }
-      const char* s = buf;
-      if (*s == '-') ++s;
-      digits.clear();
-      for (; *s && *s != 'e'; ++s)
-        if (*s >= '0' && *s <= '9') digits.push_back(*s);
-      e = std::atoi(s + 1);
+      take(buf);
+      return;
+    }
+    if (p == 1) continue;  // 1-digit neighbours are 2-digit decimals, tried at p = 2
+    // neighbours of the p-digit mantissa M (x ~ M * 10^(e - p + 1))
+    take(buf);
+    unsigned long long m = 0;
+    for (char ch : digits) m = m * 10 + (unsigned long long)(ch - '0');
+    for (size_t i = digits.size(); i < (size_t)p; ++i) m *= 10;
+    const int exp10 = e - p + 1;
+    unsigned long long lo_p = 1;
+    for (int i = 1; i < p; ++i) lo_p *= 10;  // 10^(p-1): smallest p-digit mantissa
+    long double best = 0, d;
+    unsigned long long pick = 0;
+    for (unsigned long long cand : {m - 1, m + 1}) {
+      if (cand < lo_p || cand >= lo_p * 10) continue;  // stays a p-digit decimal
+      if (reads_back(cand, exp10, x, &d) && (pick == 0 || d < best)) { best = d; pick = cand; }
+    }
+    if (pick) {
+      digits = std::to_string(pick);
+      e = exp10 + p - 1;
       while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
       return;
     }

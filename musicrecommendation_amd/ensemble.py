@@ -82,19 +82,30 @@ class DeviceEnsemble:
 
         return torch.empty(self.shape, dtype=self.torch_dtype, device=self.device)
 
+    def _after_torch(self) -> None:
+        """Order the engine's own HIP stream after everything queued so far on
+        torch's current stream (an event + hipStreamWaitEvent, no host wait):
+        inputs produced by pending torch kernels are complete and recycled
+        output allocations are no longer in use when the engine touches them.
+        Every engine call below returns after its stream has drained, so torch
+        may use the outputs right away."""
+        import torch
+
+        ext = torch.cuda.ExternalStream(self.e.stream, device=self.device)
+        ext.wait_stream(torch.cuda.current_stream(self.device))
+
     # ---- models ----------------------------------------------------------------
     def model(self, name: str):
         """ubm / ibm dense model (MR:132-307) into a new device tensor."""
-        import torch
-
         t = self.empty()
-        torch.cuda.synchronize(self.device)  # allocation visible before the engine stream writes it
+        self._after_torch()
         self.e.run_into(name, t.data_ptr())
         self.e.sync()
         return t
 
     def _combine(self, kind: int, ubm, ibm, param: float, seed: int = 0):
         out = self.empty()
+        self._after_torch()
         self.e.combine(kind, param, ubm.data_ptr(), ibm.data_ptr(), out.data_ptr(), seed=seed,
                        pair_base=self.pair_base, n_pairs=self.n_pairs)
         return out
@@ -122,6 +133,7 @@ class DeviceEnsemble:
         import torch
         import torch.distributed as dist
 
+        self._after_torch()
         mn, mx = self.e.eval_minmax(t.data_ptr())
         world = self._world()
         if world > 1:
@@ -157,5 +169,6 @@ class DeviceEnsemble:
 
     def topk(self, t) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Top-k recommendation lists of a dense device model (k = engine topk)."""
+        self._after_torch()
         self.e.topk_dense(t.data_ptr())
         return self.e.topk()

@@ -31,8 +31,12 @@ Source = Union[str, os.PathLike, Iterable[str]]
 
 
 def _as_path(src: Source, tmpdir: str, name: str) -> str:
-    if isinstance(src, (str, os.PathLike)) and os.path.exists(src):
-        return os.fspath(src)
+    """A path is used as is (and must exist: the reference's Source.fromFile
+    throws FileNotFoundException); any other iterable is a source of lines."""
+    if isinstance(src, (str, bytes, os.PathLike)):
+        if not os.path.exists(src):
+            raise FileNotFoundError(f"{os.fsdecode(src)}: no such file")
+        return os.fsdecode(src)
     path = os.path.join(tmpdir, name)
     with open(path, "w") as f:
         for line in src:  # a BufferedSource-like iterable of lines
@@ -70,18 +74,15 @@ class MusicRecommender:
         return songs, scores
 
     def _to_model(self, dense: np.ndarray) -> Model:
+        """Pair list in getModel's emission order: s-major, u-minor
+        (MR:106-108), heard songs (NaN) emit no pair (MR:109). Vectorised:
+        one nonzero over the transposed mask, names gathered as object arrays."""
         ds = self.dataset
-        sn, un = ds.song_names, ds.test_names
-        out: Model = []
-        users = [un(u) for u in range(ds.n_test)]
-        for s in range(ds.n_songs):  # s-major, u-minor (MR:106-108)
-            col = dense[:, s]
-            name = sn(s)
-            for u in range(ds.n_test):
-                x = col[u]
-                if not np.isnan(x):  # heard songs emit no pair (MR:109)
-                    out.append((users[u], (name, float(x))))
-        return out
+        s_idx, u_idx = np.nonzero(~np.isnan(dense.T))
+        users = np.array([ds.test_names(u) for u in range(ds.n_test)], dtype=object)
+        songs = np.array([ds.song_names(s) for s in range(ds.n_songs)], dtype=object)
+        vals = dense[u_idx, s_idx].astype(np.float64).tolist()
+        return list(zip(users[u_idx].tolist(), zip(songs[s_idx].tolist(), vals)))
 
     # ---- reference API (MR:132-307) -------------------------------------------
     def getUserBasedModel(self) -> Model:

@@ -23,6 +23,7 @@ KNOWN = [
     (1.7976931348623157e308, "1.7976931348623157E308"), (float("nan"), "NaN"), (float("inf"), "Infinity"),
     (float("-inf"), "-Infinity"), (0.40824829046386296, "0.40824829046386296"), (1e21, "1.0E21"),
     (9.999999999999999e-4, "9.999999999999998E-4"),
+    (2.0 ** -24, "5.960464477539063E-8"),  # asymmetric rounding interval
 ]
 
 
@@ -54,6 +55,20 @@ def test_java_double_random_round_trip_and_shortest():
         shortest = len(_digits(repr(x).replace("e", "E")))  # Python repr = shortest round trip
         assert len(_digits(s)) <= max(shortest, 2)
         assert len(_digits(s)) >= shortest or shortest == 1
+
+
+def test_java_double_powers_of_two_shortest_closest():
+    """At powers of two the rounding interval is asymmetric: the correctly
+    rounded p-digit decimal can miss while its neighbour reads back. Digits
+    must equal Python's repr (shortest, then closest: the JDK 19+ rule) for
+    every binade, apart from the 1-digit special case."""
+    for k in range(-1074, 1024):
+        x = math.ldexp(1.0, k)
+        s = java_double_string(x)
+        assert float(s) == x, (k, s)
+        ref = _digits(repr(x).replace("e", "E"))
+        if len(ref) >= 2:
+            assert _digits(s) == ref, (k, s, repr(x))
 
 
 @pytest.mark.parametrize("order", ["sorted", "emission"])
