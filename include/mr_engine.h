@@ -145,9 +145,17 @@ int mr_load(mr_ctx* ctx, const mr_dataset* d);
  * test users. The dense model of this context is n_te x (song_hi - song_lo). */
 int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
 
-/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull, 3 wide; songs
- * per LDS tile (pull: per song range) and tiles (ranges) per test user. */
+/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull, 3 wide,
+ * 4 user (auto picks fused or wide for topk <= 16, fused or separate above;
+ * pull and user only on request, see mr_options.stage1); songs per LDS tile
+ * (pull: per song range) and tiles (ranges) per test user. */
 int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int32_t* n_tiles);
+
+/* Test-user batch of the separate / wide shapes (mr_run launches the stage-1 and
+ * scoring kernels once per batch of *batch users, sized so the neighbour lists
+ * fit 8 GiB; = n_test_users for the other shapes) and the stage-1 chunking of
+ * the train users (*n_chunks chunks of *chunk users). */
+int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_chunks);
 
 /*
  * Score every (test user, song) pair of the shard for `model`, leaving the

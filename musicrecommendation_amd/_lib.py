@@ -110,6 +110,7 @@ SIGNATURES = {
     "mr_load": (c_int, [c_void_p, POINTER(MrDataset)]),
     "mr_shard_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_launch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),
     "mr_device_outputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),

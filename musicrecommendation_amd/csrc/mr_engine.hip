@@ -2666,6 +2666,15 @@ int mr_launch_info(const mr_ctx* c, int32_t* fused, int32_t* block_songs, int32_
   return MR_OK;
 }
 
+int mr_batch_info(const mr_ctx* c, int32_t* batch, int32_t* chunk, int32_t* n_chunks) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_batch_info before mr_load");
+  if (batch) *batch = c->batch;
+  if (chunk) *chunk = c->chunk;
+  if (n_chunks) *n_chunks = c->n_chunks;
+  return MR_OK;
+}
+
 }  // extern "C"
 
 namespace {

@@ -68,6 +68,10 @@ class Engine:
                    "mr_launch_info")
         self.shape = {0: "separate", 1: "fused", 2: "pull", 3: "wide", 4: "user"}[fz.value]
         self.fused, self.block_songs, self.n_tiles = self.shape == "fused", bsz.value, nt.value
+        b, ch, nch = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self._L.mr_batch_info(self._h, ctypes.byref(b), ctypes.byref(ch), ctypes.byref(nch)),
+                   "mr_batch_info")
+        self.batch, self.stage1_chunk, self.n_chunks = b.value, ch.value, nch.value
 
     # ---- lifecycle ----------------------------------------------------------
     def close(self) -> None:

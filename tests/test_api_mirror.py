@@ -2,8 +2,8 @@
 MR:12-639) end to end against the literal restatement oracle/reference_py.py:
 
 * getItemBasedModel / getUserBasedModel (MR:222-261, 132-170) return the same
-  (user, (song, score)) pairs as LiteralRecommender, scores within 1e-9
-  relative, in getModel's s-major / u-minor emission order (MR:105-111);
+  (user, (song, score)) pairs as LiteralRecommender, scores within 1e-7
+  relative (the int64 fixed-point bound the GPU parity suite uses), in getModel's s-major / u-minor emission order (MR:105-111);
 * evaluateModel (MR:636-639) equals LiteralRecommender.evaluate_model;
 * the list-shaped combination models (MR:317-481) equal the restatement's;
 * a fresh torch expression fed to the device mAP is read only after torch's
@@ -31,7 +31,9 @@ def _sources():
     yield "tiny", z["train"].tolist(), z["test"].tolist(), z["labels"].tolist()
 
 
-def _same_pairs(got, exp, tol=1e-9):
+def _same_pairs(got, exp, tol=1e-7):
+    """Same pair set; scores within the fixed-point bound of the suite (F = 32:
+    <= 2^-33 / min term relative, measured <= 5e-9 here; the north star allows 1e-5)."""
     assert len(got) == len(exp)
     g = {(u, s): x for u, (s, x) in got}
     assert len(g) == len(got), "duplicate (user, song) pair"

@@ -1,0 +1,206 @@
+"""GPU parity at the full-scale BASELINE configs (C4, C5), through the C ABI.
+
+C4 — the full Echo Nest Taste Profile shape (synth.config("c4"): 1,009,318 train
+users, 10,000 test users, 384,546 songs, ~48M rows), ItemBased
+(MR:222-261) top-10 over ALL test users on the wide launch shape:
+  * bitwise equality of songs and fixed-point keys with oracle/fixedpoint.c on
+    a fixed sample: the heaviest user (|T(u)| and listener entries), the
+    coldest user, the first and the last user of every neighbour-list batch
+    (the batch boundaries of mr_run, mr_batch_info), and seeded random users;
+  * all-user properties: keys non-increasing, ties ordered by song id, songs
+    distinct, in range, and never heard (MR:109).
+  UserBased (MR:132-170) at the same scale on a smaller sample.
+
+C5 — the ensemble config (synth.config("c5"): 2,000 test users against the
+remaining 1,017,318 train users), dense f32 ubm / ibm models on the device:
+  * sampled rows of both models bitwise equal to the oracle (cast to f32);
+  * k_combine (MR:317-481) against numpy on sampled rows, pair indices in the
+    driver's sorted order (main.scala:57-59);
+  * mr_eval_counts_device against evaluation.threshold_counts on sampled song
+    columns (MR:521-553), min / max against numpy;
+  * the mAP of the device counts (mr_eval_map) against
+    evaluation.map_from_counts (MR:588-627).
+
+Datasets are generated once per module (about a minute each on the host).
+"""
+import numpy as np
+import pytest
+import torch
+
+from musicrecommendation_amd import evaluation, synth
+from musicrecommendation_amd.engine import Engine
+from musicrecommendation_amd.ensemble import DeviceEnsemble, pair_uniform
+from oracle import native
+
+pytestmark = pytest.mark.gpu
+
+K = 10
+
+
+def _ranges(users):
+    """Sorted distinct users -> contiguous [lo, hi) runs (one oracle call each)."""
+    users = sorted(set(int(u) for u in users))
+    runs = []
+    for u in users:
+        if runs and runs[-1][1] == u:
+            runs[-1][1] = u + 1
+        else:
+            runs.append([u, u + 1])
+    return runs
+
+
+def _stage1_work(ds):
+    """Σ_{s2 ∈ T(u)} c_tr(s2) per test user: the listener entries stage 1 walks."""
+    c_tr = np.bincount(ds.tr_songs, minlength=ds.n_songs).astype(np.int64)
+    per = c_tr[ds.te_songs]
+    return np.add.reduceat(per, ds.te_off[:-1]) if per.size else np.zeros(ds.n_test, np.int64)
+
+
+def _check_topk_properties(ds, songs, keys):
+    n_te, k = songs.shape
+    free = ds.n_songs - np.diff(ds.te_off)
+    want = np.minimum(k, free)
+    valid = songs >= 0
+    assert np.array_equal(valid.sum(axis=1), want)
+    assert np.all(valid[:, :1] | ~valid[:, 1:].any(axis=1, keepdims=True))  # empty slots at the end
+    assert np.all(songs[valid] < ds.n_songs)
+    assert np.all(keys[valid] >= 0)
+    # non-increasing keys; equal keys -> ascending song id
+    kv, sv = keys[:, :-1], songs[:, :-1]
+    kn, sn = keys[:, 1:], songs[:, 1:]
+    both = valid[:, :-1] & valid[:, 1:]
+    assert np.all(~both | (kv > kn) | ((kv == kn) & (sv < sn)))
+    # distinct and never heard
+    rows = np.repeat(np.arange(n_te, dtype=np.int64), k)
+    flat = songs.reshape(-1).astype(np.int64)
+    m = flat >= 0
+    pair = rows[m] * ds.n_songs + flat[m]
+    assert np.unique(pair).size == pair.size
+    heard = np.repeat(np.arange(n_te, dtype=np.int64), np.diff(ds.te_off)) * ds.n_songs + ds.te_songs
+    assert not np.isin(pair, heard).any()
+
+
+@pytest.fixture(scope="module")
+def c4():
+    return synth.config("c4").dataset()
+
+
+@pytest.fixture(scope="module")
+def c5():
+    return synth.config("c5").dataset()
+
+
+def test_c4_ibm_all_users_top10_exact_on_sample(c4):
+    ds = c4
+    assert (ds.n_train, ds.n_test, ds.n_songs) == (1_009_318, 10_000, 384_546)
+    with Engine(ds, topk=K, dense=False) as e:
+        assert e.shape == "wide" and e.n_chunks > 1
+        e.run("ibm")
+        songs, scores, keys = e.topk()
+        batch = e.batch
+    assert 1 <= batch < ds.n_test  # several neighbour batches: their boundaries are sampled
+    _check_topk_properties(ds, songs, keys)
+    assert np.array_equal(scores, keys.view(np.float64))
+    work = _stage1_work(ds)
+    tlen = np.diff(ds.te_off)
+    sample = {int(np.argmax(tlen)), int(np.argmax(work)), int(np.argmin(work)), int(np.argmin(tlen))}
+    for b0 in range(0, ds.n_test, batch):
+        sample |= {b0, min(b0 + batch, ds.n_test) - 1}
+    sample |= set(np.random.default_rng(44).choice(ds.n_test, 6, replace=False).tolist())
+    assert len(sample) >= 16
+    for lo, hi in _ranges(sample):
+        _, ts, tk = native.fp_model(ds, "ibm", user_lo=lo, user_hi=hi, k=K, dense=False)
+        assert np.array_equal(songs[lo:hi], ts), (lo, hi)
+        assert np.array_equal(keys[lo:hi], tk), (lo, hi)
+
+
+def test_c4_ubm_top10_exact_on_sample(c4):
+    ds = c4
+    with Engine(ds, topk=K, dense=False) as e:
+        e.run("ubm")
+        songs, _scores, keys = e.topk()
+        batch = e.batch
+    _check_topk_properties(ds, songs, keys)
+    work = _stage1_work(ds)
+    sample = {0, ds.n_test - 1, batch - 1, batch, int(np.argmax(work)), int(np.argmin(work))}
+    for lo, hi in _ranges(sample):
+        _, ts, tk = native.fp_model(ds, "ubm", user_lo=lo, user_hi=hi, k=K, dense=False)
+        assert np.array_equal(songs[lo:hi], ts), (lo, hi)
+        assert np.array_equal(keys[lo:hi], tk), (lo, hi)
+
+
+def _pair_rank(ds, u):
+    """Index in the sorted model (main.scala:57-59) of every song of row u (-1 = heard)."""
+    heard = np.zeros(ds.n_songs, bool)
+    heard[ds.te_songs[ds.te_off[u]:ds.te_off[u + 1]]] = True
+    base = u * ds.n_songs - int(ds.te_off[u])
+    idx = np.full(ds.n_songs, -1, np.int64)
+    free = np.flatnonzero(~heard)
+    idx[free] = base + np.arange(free.size)
+    return idx
+
+
+def test_c5_models_combinations_and_map(c5):
+    ds = c5
+    assert (ds.n_train, ds.n_test) == (1_017_318, 2_000)
+    pos = evaluation.label_pos(ds)
+    with Engine(ds, out_dtype="f32", topk=K) as e:
+        ens = DeviceEnsemble(e, pos=pos, n_label_songs=ds.n_label_songs)
+        ubm, ibm = ens.model("ubm"), ens.model("ibm")
+        work = _stage1_work(ds)
+        rows = sorted({0, ds.n_test - 1, int(np.argmax(work)), int(np.argmin(work)), 977})
+        ub_rows, ib_rows = ubm[rows].cpu().numpy(), ibm[rows].cpu().numpy()
+        # 1) the models themselves: oracle fp64 cast to f32, bitwise (NaN = heard)
+        for j, u in enumerate(rows):
+            for name, got in (("ubm", ub_rows[j]), ("ibm", ib_rows[j])):
+                exp, _, _ = native.fp_model(ds, name, user_lo=u, user_hi=u + 1, k=K, dense=True)
+                assert np.array_equal(got, exp[0].astype(np.float32), equal_nan=True), (name, u)
+        # 2) combinations on the sampled rows
+        n_pairs = ds.n_pairs()
+        u64, i64 = ub_rows.astype(np.float64), ib_rows.astype(np.float64)
+        idx = np.stack([_pair_rank(ds, u) for u in rows])
+        cases = {
+            "linear": (ens.linear(ubm, ibm, 0.5), lambda: (u64 * 0.5 + i64 * 0.5)),
+            "aggregation": (ens.aggregation(ubm, ibm, 0.5), lambda: np.where(idx < int(0.5 * n_pairs), i64, u64)),
+        }
+        sto = ens.stochastic(ubm, ibm, 0.5, seed=1)
+        for name, (t, ref) in cases.items():
+            got = t[rows].cpu().numpy()
+            exp = ref().astype(np.float32)
+            exp[idx < 0] = np.nan
+            assert np.array_equal(got, exp, equal_nan=True), name
+        got = sto[rows].cpu().numpy()
+        cols = np.random.default_rng(5).choice(ds.n_songs, 3000, replace=False)
+        for j in range(len(rows)):
+            for s in cols:
+                if idx[j, s] < 0:
+                    assert np.isnan(got[j, s])
+                    continue
+                take = pair_uniform(1, int(idx[j, s])) < 0.5
+                assert got[j, s] == (ib_rows[j, s] if take else ub_rows[j, s])
+        del sto
+        # 3) min / max and the per-class counts on sampled song columns
+        lab = evaluation.label_matrix(ds)
+        hot = np.argsort(-pos, kind="stable")[:1000]
+        cols = np.unique(np.concatenate([hot, np.random.default_rng(6).choice(ds.n_songs, 1000, replace=False)]))
+        for name, t in (("ibm", ibm), ("linear", cases["linear"][0])):
+            mn, mx = e.eval_minmax(t.data_ptr())
+            x = t.cpu().numpy()
+            assert mn == float(np.nanmin(x)) and mx == float(np.nanmax(x)), name
+            pred, tp = e.eval_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs)
+            xc = x[:, cols].astype(np.float64)
+            with np.errstate(invalid="ignore"):
+                norm = (xc - mn) / (mx - mn)
+            for i, thr in enumerate(evaluation.THRESHOLDS):
+                with np.errstate(invalid="ignore"):
+                    p = ~np.isnan(xc) & (norm > thr)
+                assert np.array_equal(pred[cols, i], p.sum(axis=0)), (name, thr)
+                assert np.array_equal(tp[cols, i], (p & lab[:, cols]).sum(axis=0)), (name, thr)
+            # 4) the mAP fold of the device counts
+            want = evaluation.map_from_counts(pred, tp, pos, ds.n_label_songs)
+            got_map = ens.threshold_map(t)
+            assert abs(got_map - want) <= 1e-12 * max(1.0, abs(want)), (name, got_map, want)
+            del x
+        # the dense top-k of a combination model is a valid top-k of it
+        s3, _sc3, k3 = ens.topk(cases["linear"][0])
+        _check_topk_properties(ds, s3, k3)
