@@ -53,6 +53,7 @@ extern "C" {
 #define MR_E_STATE    -4 /* call out of order (e.g. mr_run before mr_load)                 */
 #define MR_E_IO       -5 /* file could not be opened/read                                  */
 #define MR_E_PARSE    -6 /* malformed TSV line (reference: scala.MatchError, MR:34)         */
+#define MR_E_RCCL     -7 /* RCCL missing or a collective failed (multi-GPU groups)          */
 
 /* ---- models ------------------------------------------------------------ */
 #define MR_UBM 0 /* UserBasedModel: MR:140-166 */
@@ -283,6 +284,74 @@ void* mr_stream(const mr_ctx* ctx);
 
 /* Thread-local description of the last error (never NULL). */
 const char* mr_last_error(void);
+
+/* ---- multi-GPU: one handle over G contexts (distributed.scala:450-479) -------
+ * The reference fans ONE driver call out over Spark partitions: by song
+ * (getItemBasedModel2 = parallelize(songs, numberSlices).map(getRanks2)
+ * .collect.flatten, distributed.scala:477-479; getUserBasedModel2 :459-461) or
+ * by test user (getItemBasedModel1 :468-470). A group is the same single call
+ * over G = n_song_shards x n_user_blocks engine contexts: context (b, g) scores
+ * test-user block b (contiguous, sizes within one) over song-range shard g
+ * (boundaries balance sum(c_tr(s) + 1), the stage-2 work) on its own GPU and
+ * stream. The shards of a user block then exchange their per-user top-k lists
+ * with ONE all-gather and merge them by (key desc, song asc): the results are
+ * bit-identical to one context (fixed-point keys) for every layout.
+ * Transports: MR_TRANSPORT_RCCL — every context on its own device, one RCCL
+ * communicator per user block (ncclCommInitAll, owned by the group; librccl is
+ * loaded on first use), ncclAllGather under ncclGroupStart/End on the
+ * contexts' streams, the merge on every device; MR_TRANSPORT_COPY — every
+ * context on ONE device (logical shards), the block's first context gathers
+ * with device copies and merges. AUTO = RCCL when the contexts span >= 2
+ * devices. A group is driven by one host thread; calls are synchronous unless
+ * stated. */
+#define MR_TRANSPORT_AUTO 0
+#define MR_TRANSPORT_COPY 1
+#define MR_TRANSPORT_RCCL 2
+
+typedef struct mr_group_options {
+  int32_t n_song_shards;  /* G_s >= 1 (default 1) */
+  int32_t n_user_blocks;  /* G_u >= 1 (default 1) */
+  int32_t transport;      /* MR_TRANSPORT_* (default AUTO) */
+  int32_t n_devices;      /* entries of `devices`; 0 = every context on opt->device */
+  const int32_t* devices; /* context i = b*G_s + g runs on devices[i % n_devices] (not retained) */
+} mr_group_options;
+
+typedef struct mr_group mr_group;
+
+/* Host helper (no GPU): the group's song-range shard boundaries, bounds[0..n_shards]
+ * (bounds[0] = 0, bounds[n_shards] = n_songs), balancing sum(c_tr(s) + 1). */
+int mr_song_shards(const mr_dataset* d, int32_t n_shards, int32_t* bounds);
+
+int mr_group_options_default(mr_group_options* gopt);
+/* opt: the contexts' options (song_lo/song_hi must be 0: the group sets them). */
+int mr_group_create(const mr_options* opt, const mr_group_options* gopt, mr_group** out);
+int mr_group_destroy(mr_group* g);
+/* Split the dataset (shards, user blocks) and load every context (in parallel). */
+int mr_group_load(mr_group* g, const mr_dataset* d);
+/* Geometry of context i after mr_group_load: songs [*song_lo, *song_hi), test
+ * users [*user_lo, *user_hi), device. */
+int mr_group_info(const mr_group* g, int32_t i, int32_t* song_lo, int32_t* song_hi, int32_t* user_lo,
+                  int32_t* user_hi, int32_t* device);
+int mr_group_transport(const mr_group* g, int32_t* transport);
+/* Borrowed context i (e.g. for mr_timing_begin/end on its stream); NULL on error. */
+mr_ctx* mr_group_context(mr_group* g, int32_t i);
+/* Score every pair on every context, then the top-k exchange (asynchronous on
+ * the contexts' streams; mr_group_sync waits for all of them). */
+int mr_group_run(mr_group* g, int model);
+int mr_group_sync(mr_group* g);
+/* Merged top-k of all test users (n_test x k, host), after mr_group_run / in one call. */
+int mr_group_copy_topk(mr_group* g, int32_t* songs, double* scores, int64_t* keys);
+int mr_group_topk(mr_group* g, int model, int k, int32_t* songs, double* scores, int64_t* keys);
+/* Device pointers of the merged lists held by context i (rows of its user
+ * block; COPY: the block's first context holds them). */
+int mr_group_device_topk(mr_group* g, int32_t i, int32_t** songs, int64_t** keys, double** scores);
+/* The dense model n_test x n_songs on the host (collect.flatten, distributed.scala:478). */
+int mr_group_copy_dense(mr_group* g, void* out);
+int mr_group_score_dense(mr_group* g, int model, void* out);
+/* All-gather of the dense shards: dst[i] = device buffer on context i's device
+ * of (user_hi - user_lo) x n_songs elements, filled with its block's full rows
+ * (RCCL: ncclAllGather of equal padded shard blocks + strided on-device copies). */
+int mr_group_allgather_dense(mr_group* g, void* const* dst);
 
 /* ---- host ingest: TSV triplets -> interned corpus (extractData, MR:26-91) ---- */
 typedef struct mr_corpus mr_corpus;

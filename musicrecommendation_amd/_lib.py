@@ -27,6 +27,8 @@ MR_E_OOM = -3
 MR_E_STATE = -4
 MR_E_IO = -5
 MR_E_PARSE = -6
+MR_E_RCCL = -7
+MR_TRANSPORT_AUTO, MR_TRANSPORT_COPY, MR_TRANSPORT_RCCL = 0, 1, 2
 MR_UBM = 0
 MR_IBM = 1
 MR_OUT_F32 = 0
@@ -39,6 +41,7 @@ _ERRNAMES = {
     MR_E_STATE: "MR_E_STATE",
     MR_E_IO: "MR_E_IO",
     MR_E_PARSE: "MR_E_PARSE",
+    MR_E_RCCL: "MR_E_RCCL",
 }
 
 
@@ -74,6 +77,16 @@ class MrOptions(ctypes.Structure):
         ("train_order", c_int32),
         ("topk_lists", c_int32),
         ("reserved", c_int32 * 3),
+    ]
+
+
+class MrGroupOptions(ctypes.Structure):
+    _fields_ = [
+        ("n_song_shards", c_int32),
+        ("n_user_blocks", c_int32),
+        ("transport", c_int32),
+        ("n_devices", c_int32),
+        ("devices", POINTER(c_int32)),
     ]
 
 
@@ -144,6 +157,23 @@ SIGNATURES = {
     "mr_model_write_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32]),
     "mr_model_read_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "mr_java_double_string": (c_int, [c_double, c_char_p, c_int32]),
+    "mr_song_shards": (c_int, [POINTER(MrDataset), c_int32, c_void_p]),
+    "mr_group_options_default": (c_int, [POINTER(MrGroupOptions)]),
+    "mr_group_create": (c_int, [POINTER(MrOptions), POINTER(MrGroupOptions), POINTER(c_void_p)]),
+    "mr_group_destroy": (c_int, [c_void_p]),
+    "mr_group_load": (c_int, [c_void_p, POINTER(MrDataset)]),
+    "mr_group_info": (c_int, [c_void_p, c_int32, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
+                              POINTER(c_int32), POINTER(c_int32)]),
+    "mr_group_transport": (c_int, [c_void_p, POINTER(c_int32)]),
+    "mr_group_context": (c_void_p, [c_void_p, c_int32]),
+    "mr_group_run": (c_int, [c_void_p, c_int]),
+    "mr_group_sync": (c_int, [c_void_p]),
+    "mr_group_copy_topk": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mr_group_topk": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "mr_group_device_topk": (c_int, [c_void_p, c_int32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),
+    "mr_group_copy_dense": (c_int, [c_void_p, c_void_p]),
+    "mr_group_score_dense": (c_int, [c_void_p, c_int, c_void_p]),
+    "mr_group_allgather_dense": (c_int, [c_void_p, c_void_p]),
 }
 
 _lib = None

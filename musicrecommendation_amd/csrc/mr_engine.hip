@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "mr_engine.h"
+#include "mr_internal.h"
 
 
 namespace {
@@ -2822,6 +2823,35 @@ int run_model(mr_ctx* c, int model) {
 
 }  // namespace
 
+namespace mr_internal {
+
+int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
+  if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
+  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
+                 reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
+  const int lds = merge_lds_bytes(k);
+  if (lds > 160 * 1024) return fail(MR_E_INVALID, "merge of %d lists x %d needs too much LDS", n_shards, k);
+  MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  for (int y0 = 0; y0 < n_te; y0 += 65535) {
+    MergeParams q = mp;
+    q.keys += (size_t)y0 * k;
+    q.songs += (size_t)y0 * k;
+    q.out_keys += (size_t)y0 * k;
+    q.out_songs += (size_t)y0 * k;
+    if (q.out_scores) q.out_scores += (size_t)y0 * k;
+    hipLaunchKernelGGL(k_topk_merge, dim3(std::min(65535, n_te - y0)), dim3(kThreads), lds, c->stream, q);
+  }
+  MR_HIP(hipGetLastError());
+  return MR_OK;
+}
+
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+}  // namespace mr_internal
+
 extern "C" {
 
 int mr_run(mr_ctx* c, int model) {
@@ -2905,16 +2935,8 @@ int mr_topk(mr_ctx* c, int model, int k, int32_t* songs, double* scores, int64_t
 int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
                          const int64_t* keys_in, const double* /*scores_in*/, int32_t* songs_out,
                          int64_t* keys_out, double* scores_out) {
-  if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
-  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
-  MR_HIP(hipSetDevice(c->opt.device));
-  MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
-                 reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
-  const int lds = merge_lds_bytes(k);
-  if (lds > 160 * 1024) return fail(MR_E_INVALID, "merge of %d lists x %d needs too much LDS", n_shards, k);
-  MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  hipLaunchKernelGGL(k_topk_merge, dim3(n_te), dim3(kThreads), lds, c->stream, mp);
-  MR_HIP(hipGetLastError());
+  const int rc = mr_internal::merge_async(c, n_shards, n_te, k, songs_in, keys_in, songs_out, keys_out, scores_out);
+  if (rc) return rc;
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
 }

@@ -1,0 +1,22 @@
+// mr_internal.h — entry points shared between the engine's translation units
+// (not part of the C ABI in include/mr_engine.h).
+#ifndef MR_INTERNAL_H
+#define MR_INTERNAL_H
+
+#include <stdint.h>
+
+#include "mr_engine.h"
+
+namespace mr_internal {
+
+// k_topk_merge of n_shards [shard][n_te][k] device lists into [n_te][k] outputs,
+// enqueued on the context's stream (no host wait).
+int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out);
+
+// Set the calling thread's mr_last_error() message; returns code.
+int set_error(int code, const char* msg);
+
+}  // namespace mr_internal
+
+#endif  // MR_INTERNAL_H

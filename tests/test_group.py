@@ -1,0 +1,136 @@
+"""Multi-GPU behind the C ABI (mr_group_*, the reference's getItemBasedModel2 /
+getUserBasedModel2 fan-out, distributed.scala:459-479).
+
+CPU: the shard boundaries of the library (mr_song_shards) equal
+sharding.song_shards (Σ(c_tr + 1) balance); creating a group without a GPU
+fails with an error code (never a crash or a CPU fallback).
+GPU (one MI355X): G = song shards x user blocks logical contexts on device 0
+(COPY transport: device-copy exchange) give top-k lists, keys and dense models
+bit-identical to one context, for ubm and ibm; the dense all-gather assembles
+full rows on every context; a 1-context RCCL group runs the real
+ncclCommInitAll / ncclAllGather / merge sequence. With >= 2 GPUs visible the
+RCCL transport takes over (not reachable on the 1-GPU box: RCCL refuses two
+ranks on one device)."""
+import numpy as np
+import pytest
+
+from musicrecommendation_amd import _lib, synth
+from musicrecommendation_amd.group import Group, song_shards_native
+from musicrecommendation_amd.sharding import song_shards
+
+from helpers import kat, dataset_from_lines, synth_fixture
+
+
+def _datasets():
+    K = kat()
+    yield "kat", dataset_from_lines(K["train"], K["test"], K["labels"])
+    yield "small", synth_fixture("small")[0]
+    yield "c2x24", synth.config("c2", n_test=24).dataset()
+
+
+def test_native_song_shards_equal_python_rule():
+    for name, ds in _datasets():
+        for n in range(1, min(9, ds.n_songs) + 1):
+            assert song_shards_native(ds, n) == song_shards(ds, n), (name, n)
+
+
+def test_group_without_gpu_fails_cleanly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    ds = synth_fixture("tiny")[0]
+    with pytest.raises(_lib.EngineError) as e:
+        Group(ds, song_shards=2)
+    assert e.value.code in (_lib.MR_E_HIP, _lib.MR_E_INVALID)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [(2, 1), (3, 1), (1, 2), (2, 2), (3, 2)])
+def test_copy_group_equals_one_context(layout):
+    from musicrecommendation_amd.engine import Engine
+
+    gs, gu = layout
+    for name, ds in _datasets():
+        if ds.n_songs < gs or ds.n_test < gu:
+            continue
+        with Engine(ds, out_dtype="f64", topk=7) as e:
+            ref = {}
+            for model in ("ibm", "ubm"):
+                e.run(model)
+                ref[model] = (e.dense(), *e.topk())
+        with Group(ds, song_shards=gs, user_blocks=gu, out_dtype="f64", topk=7) as g:
+            assert g.transport == "copy" and len(g.layout) == gs * gu
+            shards = song_shards(ds, gs)
+            for i, (slo, shi, ulo, uhi, dev) in enumerate(g.layout):
+                assert (slo, shi) == shards[i % gs] and dev == 0
+            for model in ("ibm", "ubm"):
+                g.run(model)
+                songs, scores, keys = g.topk()
+                d_ref, s_ref, sc_ref, k_ref = ref[model]
+                assert np.array_equal(songs, s_ref), (name, layout, model)
+                assert np.array_equal(keys, k_ref), (name, layout, model)
+                assert np.array_equal(scores, sc_ref, equal_nan=True), (name, layout, model)
+                assert np.array_equal(g.dense(), d_ref, equal_nan=True), (name, layout, model)
+
+
+@pytest.mark.gpu
+def test_copy_group_dense_allgather_and_repeated_runs():
+    import torch
+
+    ds = synth.config("c2", n_test=24).dataset()
+    from musicrecommendation_amd.engine import Engine
+
+    with Engine(ds, out_dtype="f32", topk=10) as e:
+        e.run("ibm")
+        d_ref = e.dense()
+        s_ref = e.topk()[0]
+    with Group(ds, song_shards=3, user_blocks=2, out_dtype="f32", topk=10) as g:
+        for _ in range(3):  # back-to-back runs without host syncs in between
+            g.run("ubm")
+            g.run("ibm")
+        g.sync()
+        assert np.array_equal(g.topk()[0], s_ref)
+        bufs = [torch.empty((uhi - ulo, ds.n_songs), dtype=torch.float32, device="cuda")
+                for (_slo, _shi, ulo, uhi, _d) in g.layout]
+        torch.cuda.synchronize()
+        g.allgather_dense([b.data_ptr() for b in bufs])
+        for (slo, shi, ulo, uhi, _d), b in zip(g.layout, bufs):
+            assert np.array_equal(b.cpu().numpy(), d_ref[ulo:uhi], equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dense", [True, False])
+def test_rccl_group_single_device(dense):
+    """The RCCL transport end to end on one GPU: a 1-rank communicator, the
+    all-gather of the lists (and of the dense shard), the merge kernel."""
+    import torch
+    from musicrecommendation_amd.engine import Engine
+
+    ds = synth.config("c2", n_test=24).dataset()
+    with Engine(ds, out_dtype="f32", topk=10, dense=dense) as e:
+        e.run("ibm")
+        s_ref, sc_ref, k_ref = e.topk()
+        d_ref = e.dense() if dense else None
+    with Group(ds, transport="rccl", out_dtype="f32", topk=10, dense=dense) as g:
+        assert g.transport == "rccl"
+        g.run("ibm")
+        songs, scores, keys = g.topk()
+        assert np.array_equal(songs, s_ref) and np.array_equal(keys, k_ref)
+        if dense:
+            assert np.array_equal(g.dense(), d_ref, equal_nan=True)
+            b = torch.empty((ds.n_test, ds.n_songs), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            g.allgather_dense([b.data_ptr()])
+            assert np.array_equal(b.cpu().numpy(), d_ref, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_group_errors():
+    ds = synth_fixture("tiny")[0]
+    with pytest.raises(_lib.EngineError):
+        Group(ds, song_shards=2, transport="rccl")  # two contexts, one device
+    with pytest.raises(_lib.EngineError):
+        Group(ds, song_shards=ds.n_songs + 1)
+    with pytest.raises(_lib.EngineError):
+        Group(ds, user_blocks=ds.n_test + 1)
