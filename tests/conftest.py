@@ -30,6 +30,7 @@ def _built():
         if not os.path.exists(b.OUT):
             raise
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "jni"), "harness"], check=True)
 
 TESTS = os.path.dirname(os.path.abspath(__file__))
 if TESTS not in sys.path:
