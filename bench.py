@@ -8,12 +8,18 @@ score written to HBM as fp32) and stage 3 (top-10 per test user) — what the
 reference's getItemBasedModel computes (MusicRecommender.scala MR:222-261),
 plus the recommendation list.
 
-Multi-GPU (one process per GPU, torchrun): weak scaling over test-user blocks —
+Multi-GPU (one process per GPU, torchrun) — the layout the driver's N>1 run
+measures is the default ``--shard users``: weak scaling over test-user blocks,
 rank r scores test users [10r, 10r+10) of a 500 x 10N dataset over all songs
-(an exact partition of the model's pairs; no data-path collective). With
-``--shard songs`` the north star's song-range layout runs instead (every rank
-scores 10N test users on its song range, then one RCCL all-gather of the
-top-k lists + merge).
+(an exact partition of the model's pairs; no data-path collective). C2 is
+launch-latency-bound (one 18 us kernel per step), so any exchange would only
+add latency there ("C2 is too small to scale"). ``--shard
+songs`` runs the north star's song-range layout (every rank scores 10N test
+users on its song range, then one RCCL all-gather of the top-k lists + the
+device merge), ``--shard 2d --song-groups G_s`` the 2-D product (G_s song
+shards x N/G_s user blocks, the all-gather inside each block) — the layouts
+for the full-scale configs (``--config c4`` / ``c5``: strong scaling over the
+fixed test set; DESIGN.md §6 has the Amdahl table).
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the byte model.
 """
@@ -38,6 +44,8 @@ from musicrecommendation_amd.engine import Engine  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 SCALA_PAR_PAIRS_PER_S = 508.0  # ibm par 500/10/16,785 = 330,385 ms (README.md:106)
+SCALA_C1_UBM_SEQ_PAIRS_PER_S = 1120.0  # ubm seq 100/10/4,798 = 42,857 ms (README.md:72)
+README_C1_MS = {"ubm": 42857, "ibm": 70839}  # README.md:72 (sequential, 100/10)
 TEST_PER_GPU = 10
 
 
@@ -80,13 +88,33 @@ def kernel_bytes(ab, fused: bool):
     return {"neighbours": ab["neighbours"], "score": ab["score"] + ab["merge"]}
 
 
+def host_cores():
+    """CPU threads this process can really use: the affinity mask, capped by a
+    cgroup CPU quota when one is set (on the GPU box os.cpu_count() shows the
+    whole machine while the job gets a share of it)."""
+    n = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota))) if quota else aff
+    return {"nproc": n, "affinity": aff, "cgroup_cpu_quota": quota, "threads": usable}
+
+
 def cpu_baseline(ds, model: str, seconds: float):
     """Literal restatement of getItemBasedModelP (oracle/literal.c, string ids,
-    linear contains, pthreads over songs x users like MR:119-125) timed on a
-    bounded block of the s-major pair enumeration."""
+    linear contains, pthreads over songs x users like MR:119-125) on all the
+    host cores this job can use, timed on a bounded block of the s-major pair
+    enumeration."""
     from oracle import native
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    host = host_cores()
+    threads = host["threads"]
     tr, te, _ = native.dataset_lines(ds)
     li = native.LiteralInputs(tr, te)
     total = ds.n_songs * ds.n_test
@@ -99,9 +127,29 @@ def cpu_baseline(ds, model: str, seconds: float):
     _, emitted = li.model(model, threads=threads, pair_lo=0, pair_hi=n)
     dt = time.perf_counter() - t0
     return {
-        "value": emitted / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-        "sample": f"oracle/literal.c {model}: first {n} of {total} (song, user) pairs of the C2 "
-                  f"enumeration ({emitted} scored), {dt:.1f} s",
+        "value": emitted / dt, "unit": "pairs/s", "cores": threads, "kind": "port", "host": host,
+        "sample": f"oracle/literal.c {model} (getModelP, {threads} threads): first {n} of {total} (song, user) "
+                  f"pairs of the enumeration ({emitted} scored), {dt:.1f} s",
+    }
+
+
+def cpu_baseline_sequential(ds, model: str):
+    """Config 1 is the reference's SEQUENTIAL Scala path (getUserBasedModel,
+    MR:132-170, README.md:72 = 42,857 ms on an i5-8250U): the literal loop nest
+    (oracle/literal.c) on one thread over the WHOLE model, timed end to end."""
+    from oracle import native
+
+    tr, te, _ = native.dataset_lines(ds)
+    li = native.LiteralInputs(tr, te)
+    t0 = time.perf_counter()
+    _, emitted = li.model(model, threads=1)
+    dt = time.perf_counter() - t0
+    return {
+        "value": emitted / dt, "unit": "pairs/s", "cores": 1, "kind": "port", "model_ms": dt * 1e3,
+        "sample": f"oracle/literal.c {model} getModel (sequential): the whole model, {emitted} pairs, "
+                  f"{dt * 1e3:.0f} ms",
+        "reference_published": {"model_ms": README_C1_MS.get(model), "source": "README.md:72",
+                                "hardware": "Intel i5-8250U (README.md:62), Scala 2.12 sequential"},
     }
 
 
@@ -139,17 +187,22 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     """Config 5: the reference's whole evaluation pipeline on device — ubm + ibm
     dense models, linear / aggregation / stochastic combinations (main.scala:57-89,
     MR:317-481) and the threshold mAP of all five (MR:636), 2,000 test users
-    against the full train set. N > 1: song-range shards (the north star's
-    layout); combinations are per pair, the mAP reductions go over RCCL."""
+    against the full train set. N > 1: the 2-D layout of sharding.ShardScorer
+    (--shard songs: song shards only; users: test-user blocks only); combinations
+    are per pair, the mAP reductions (MIN/MAX, count SUM) go over RCCL."""
     from musicrecommendation_amd import evaluation
     from musicrecommendation_amd.ensemble import DeviceEnsemble
-    from musicrecommendation_amd.sharding import song_shards
+    from musicrecommendation_amd.sharding import layout_2d, song_shards, user_blocks
 
     n_tr, n_te, _seed = synth.BULK_CONFIGS["c5"]
-    ds = synth.config("c5").dataset()
-    lo, hi = song_shards(ds, world)[rank] if world > 1 else (0, ds.n_songs)
+    full = synth.config("c5").dataset()
+    gs, gu = layout_2d(world, song_groups_for(args, world))
+    a, b = user_blocks(full.n_test, gu)[rank // gs]
+    lo, hi = song_shards(full, gs)[rank % gs]
+    ds = full if gu == 1 else full.subset_test_users(a, b)
     eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi)
-    ens = DeviceEnsemble(eng, pos=evaluation.label_pos(ds), n_label_songs=ds.n_label_songs)
+    ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),
+                         pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs)
     maps = {}
 
     def step():
@@ -180,12 +233,12 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
     if rank == 0:
-        pairs = ds.n_pairs()
+        pairs = full.n_pairs()
         value = pairs * args.steps / elapsed
-        songs, _sc, _k = ens.topk(models["lcm"])  # this rank's shard when world > 1
-        ab = algorithmic_bytes(ds, 4, 10)
+        songs, _sc, _k = ens.topk(models["lcm"])  # this rank's cell when world > 1
+        ab = algorithmic_bytes(full, 4, 10)
         model_bytes = sum(ab.values())
-        dense_elems = ds.n_test * ds.n_songs
+        dense_elems = full.n_test * full.n_songs
         # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)
         step_bytes = 2 * model_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
         step_s = elapsed / args.steps
@@ -195,23 +248,73 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
             "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (bulk Zipf/lognormal Taste-Profile-shaped triplets, capped head, SURVEY.md §8d)",
-            "config": {"workload": f"c5: {n_tr} train / {n_te} test / {ds.n_songs} songs; ubm + ibm dense fp32, "
+            "config": {"workload": f"c5: {n_tr} train / {n_te} test / {full.n_songs} songs; ubm + ibm dense fp32, "
                                    f"linear(0.5) + aggregation(0.5) + stochastic(0.5, seed 1), threshold mAP x5",
-                       "n_train": n_tr, "n_test": n_te, "n_songs": ds.n_songs, "pairs_per_step": pairs,
-                       "parallelism": f"songs{world}"},
+                       "n_train": n_tr, "n_test": n_te, "n_songs": full.n_songs, "pairs_per_step": pairs,
+                       "parallelism": f"songs{gs}xusers{gu}"},
             "roofline": {"bound": "hbm", "kernel": "whole step (2 scoring passes + 3 combinations + 5 evaluations)",
                          "achieved": step_bytes / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
                          "algorithmic_bytes_per_step": step_bytes},
             "threshold_mAP": maps,
-            "mAP@10_lcm": evaluation.map_at_k(songs, ds, 10) if world == 1 else None,
-            "cpu_baseline": (cpu_baseline_twohop(ds, "ibm", args.cpu_baseline_seconds)
+            "mAP@10_lcm": evaluation.map_at_k(songs, full, 10) if world == 1 else None,
+            "cpu_baseline": (cpu_baseline_twohop(full, "ibm", args.cpu_baseline_seconds)
                              if world == 1 and not args.no_cpu_baseline else None),
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def song_groups_for(args, world: int) -> int:
+    """G_s of the layout: --shard songs -> world, users -> 1, 2d -> --song-groups
+    (default 2 when it divides world, else world)."""
+    if args.shard == "songs":
+        return world
+    if args.shard == "users":
+        return 1
+    if args.song_groups:
+        return args.song_groups
+    return 2 if world % 2 == 0 else world
+
+
+def end_to_end(ds, model: str, reps: int = 3):
+    """The reference's whole call chain on one GPU, wall clock: ingest of the
+    three TSV files (native reader, ≙ the constructor MR:26-91) -> mr_load
+    (host-side index build + H2D) -> mr_run -> D2H of the dense fp32 model
+    (≙ getModel's result array, MR:105-111). Median of `reps` runs; the files
+    are written once beforehand (untimed)."""
+    import tempfile
+
+    from musicrecommendation_amd.dataset import Dataset
+
+    rows = []
+    with tempfile.TemporaryDirectory() as td:
+        paths = [os.path.join(td, n) for n in ("train.txt", "test.txt", "labels.txt")]
+        ds.write_tsv(*paths)
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d2 = Dataset.from_tsv(*paths)
+            t1 = time.perf_counter()
+            e = Engine(d2, device=torch.cuda.current_device(), out_dtype="f32", topk=10)
+            t2 = time.perf_counter()
+            e.run(model)
+            e.sync()
+            t3 = time.perf_counter()
+            dense = e.dense()
+            t4 = time.perf_counter()
+            e.close()
+            rows.append((t4 - t0, t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+    rows.sort()
+    tot, ing, load, run, d2h = rows[len(rows) // 2]
+    return {"ms": tot * 1e3, "pairs_per_s": ds.n_pairs() / tot,
+            "breakdown_ms": {"ingest_tsv": ing * 1e3, "mr_load_index_h2d": load * 1e3, "mr_run": run * 1e3,
+                             "d2h_dense": d2h * 1e3},
+            "d2h_bytes": int(dense.nbytes),
+            "note": "wall clock, one GPU: native TSV ingest + mr_load (host index build + H2D) + mr_run + "
+                    "D2H of the dense fp32 model; median of 3 (value excludes all of this but the kernels)"}
 
 
 def main() -> None:
@@ -221,7 +324,11 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--model", default="ibm", choices=["ibm", "ubm"])
-    ap.add_argument("--shard", default="users", choices=["users", "songs"])
+    ap.add_argument("--shard", default="users", choices=["users", "songs", "2d"],
+                    help="N > 1 layout: test-user blocks (default), song-range shards + all-gather of the "
+                         "top-k lists (north star), or the 2-D product of both (--song-groups)")
+    ap.add_argument("--song-groups", type=int, default=0, help="2d: song shards per user block")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (ingest + H2D + D2H) timing")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
@@ -260,26 +367,10 @@ def main() -> None:
     else:
         n_tr, n_te, _seed, _t = synth.CONFIGS[args.config]
     dense_out = not bulk
-    if args.shard == "users" and bulk:
-        # strong scaling: rank r scores test users [n_te r / N, n_te (r+1) / N)
-        full = synth.config(args.config).dataset()
-        lo, hi = n_te * rank // world, n_te * (rank + 1) // world
-        blocks = [full.subset_test_users(lo, hi)]
-        engines = [Engine(blocks[0], device=local, out_dtype="f32", topk=10, dense=False, stage1=args.stage1)]
-        ds = blocks[0]
-        eng = engines[0]
-        pairs_per_engine = [blocks[0].n_pairs()]
-        step_i = [0]
-
-        def step():
-            engines[0].run(args.model)
-            step_i[0] += 1
-
-        def drain():
-            engines[0].sync()
-    elif args.shard == "users":
-        # rank r, in-flight slot j scores test-user block (r * inflight + j) of a
-        # 500 x (10 * world * inflight) dataset: disjoint blocks, same train set
+    if args.shard == "users" and not bulk:
+        # weak scaling: rank r, in-flight slot j scores test-user block
+        # (r * inflight + j) of a 500 x (10 * world * inflight) dataset: disjoint
+        # blocks, same train set, no data-path collective
         nb = world * args.inflight
         full = synth.config(args.config, n_test=n_te * nb).dataset()
         blocks = [full.subset_test_users(b * n_te, (b + 1) * n_te)
@@ -298,25 +389,36 @@ def main() -> None:
         def drain():
             for e in engines:
                 e.sync()
-    else:
-        from musicrecommendation_amd.sharding import SongShardScorer
 
-        full = ds = synth.config(args.config, n_test=None if bulk else n_te * world).dataset()
-        scorer = SongShardScorer(ds, rank, world, local, topk=10, out_dtype="f32", dense=dense_out)
+        def rank_pairs(k):
+            return float(sum(pairs_per_engine[i % len(engines)] for i in range(k)))
+    else:
+        # 2-D layout (sharding.ShardScorer): user blocks x song shards with one
+        # all-gather of the top-k lists per block. bulk: strong scaling over the
+        # fixed test set; small configs: weak, 10 test users per GPU in total.
+        from musicrecommendation_amd.sharding import ShardScorer
+
+        full = synth.config(args.config, n_test=None if bulk else n_te * world).dataset()
+        scorer = ShardScorer(full, rank, world, local, song_groups=song_groups_for(args, world), topk=10,
+                             out_dtype="f32", dense=dense_out, stage1=args.stage1)
         eng = scorer.engine
-        heard = ds.heard_mask()[:, eng.song_lo:eng.song_hi]
-        pairs_rank = int(heard.size - heard.sum())
+        ds = scorer.ds
+        engines = [eng]
+        pr = scorer.pairs()
 
         def step():
             scorer.step(args.model)
 
         def drain():
-            eng.sync()
+            scorer.sync()
+
+        def rank_pairs(k):
+            return float(pr) * k
 
     for _ in range(args.warmup):
         step()
     drain()
-    if args.shard == "users":
+    if args.shard == "users" and not bulk:
         step_i[0] = 0
     if world > 1:
         dist.barrier()
@@ -331,10 +433,7 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if args.shard == "users":  # pairs scored by this rank over the timed steps
-        pairs_total_rank = float(sum(pairs_per_engine[i % len(engines)] for i in range(args.steps)))
-    else:
-        pairs_total_rank = float(pairs_rank) * args.steps
+    pairs_total_rank = rank_pairs(args.steps)  # pairs scored by this rank over the timed steps
     stats = torch.tensor([elapsed, pairs_total_rank], dtype=torch.float64, device="cuda")
     if world > 1:
         t_max = stats[:1].clone()
@@ -373,13 +472,13 @@ def main() -> None:
         # quality companions on the last step's outputs (host-side, untimed)
         from musicrecommendation_amd import evaluation
 
-        if args.shard == "users":
+        if args.shard == "users" and not bulk:
             songs, _sc, _k = eng.topk()
             map10 = evaluation.map_at_k(songs, ds, 10)
             ref_map = evaluation.threshold_map(eng.dense().astype(np.float64), ds) if dense_out else None
         else:
             s_, _k = scorer.topk()
-            map10 = evaluation.map_at_k(s_, ds, 10)
+            map10 = evaluation.map_at_k(s_, ds, 10)  # this rank's user block
             ref_map = None
         line = {
             "metric": "scored (test-user,song) pairs/sec, ItemBasedModel, 1/2/4/8 MI355X + mAP@10"
@@ -401,7 +500,9 @@ def main() -> None:
                             f"{full.n_songs} songs, {'fp32 dense scores + ' if dense_out else ''}top-10, "
                             f"shard={args.shard}",
                 "n_train": n_tr, "n_test": full.n_test, "n_songs": full.n_songs,
-                "pairs_per_step": pairs_all / args.steps, "parallelism": f"{args.shard}{world}",
+                "pairs_per_step": pairs_all / args.steps,
+                "parallelism": (f"users{world}" if args.shard == "users" and not bulk
+                                else f"songs{scorer.gs}xusers{scorer.gu}"),
                 "inflight": args.inflight,
             },
             "roofline": {
@@ -429,17 +530,23 @@ def main() -> None:
             "mAP@10": map10,
             "ref_threshold_mAP": ref_map,
         }
+        if args.config == "c1":  # config 1 names the reference's sequential Scala path
+            line["vs_baseline"] = value / SCALA_C1_UBM_SEQ_PAIRS_PER_S if args.model == "ubm" else None
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = (cpu_baseline_twohop(ds, args.model, args.cpu_baseline_seconds) if bulk
-                                    else cpu_baseline(ds, args.model, args.cpu_baseline_seconds))
+            if bulk:
+                line["cpu_baseline"] = cpu_baseline_twohop(ds, args.model, args.cpu_baseline_seconds)
+            elif args.config == "c1":
+                line["cpu_baseline"] = cpu_baseline_sequential(ds, args.model)
+                line["cpu_baseline_par"] = cpu_baseline(ds, args.model, args.cpu_baseline_seconds)
+            else:
+                line["cpu_baseline"] = cpu_baseline(ds, args.model, args.cpu_baseline_seconds)
         else:
             line["cpu_baseline"] = None
+        if world == 1 and not bulk and not args.no_e2e:
+            line["end_to_end"] = end_to_end(ds, args.model)
         print(json.dumps(line), flush=True)
-    if args.shard == "users":
-        for e in engines:
-            e.close()
-    else:
-        eng.close()
+    for e in engines:
+        e.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -212,6 +212,10 @@ int mr_copy_topk(mr_ctx* ctx, int32_t* songs, double* scores, int64_t* keys);
 /* Same, into DEVICE buffers of the context's GPU (e.g. an all-gather send
  * buffer owned by the caller); stream-ordered, returns after completion. */
 int mr_copy_topk_device(mr_ctx* ctx, int32_t* songs, int64_t* keys);
+/* Same, enqueued on the context stream without waiting (stream-ordered after
+ * the last mr_run; the caller orders its own stream after it, e.g. with an
+ * event — the one-process-per-GPU exchange of sharding.py). */
+int mr_copy_topk_device_async(mr_ctx* ctx, int32_t* songs, int64_t* keys);
 
 /*
  * Merge per-shard top-k lists (G shards, each n_te x k, song ids global) into
@@ -225,6 +229,9 @@ int mr_topk_merge_host(int32_t n_shards, int32_t n_te, int32_t k,
 int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
                          const int32_t* songs_in, const int64_t* keys_in, const double* scores_in,
                          int32_t* songs_out, int64_t* keys_out, double* scores_out);
+/* The device merge enqueued on the context stream without waiting. */
+int mr_topk_merge_device_async(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                               const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out);
 
 /* ---- combination models and evaluation on the device (MR:317-481, MR:521-639) ----
  * Over dense models of the context's shard (device pointers, n_te x width of

@@ -2918,6 +2918,22 @@ int mr_copy_topk_device(mr_ctx* c, int32_t* songs, int64_t* keys) {
   return MR_OK;
 }
 
+int mr_copy_topk_device_async(mr_ctx* c, int32_t* songs, int64_t* keys) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_copy_topk_device_async before mr_load");
+  if (c->opt.topk <= 0) return fail(MR_E_STATE, "context created with topk=0");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const size_t n = (size_t)c->n_te * c->opt.topk;
+  if (songs) MR_HIP(hipMemcpyAsync(songs, c->top_song.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (keys) MR_HIP(hipMemcpyAsync(keys, c->top_key.p, n * 8, hipMemcpyDeviceToDevice, c->stream));
+  return MR_OK;
+}
+
+int mr_topk_merge_device_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                               const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
+  return mr_internal::merge_async(c, n_shards, n_te, k, songs_in, keys_in, songs_out, keys_out, scores_out);
+}
+
 int mr_score_dense(mr_ctx* c, int model, void* out) {
   int rc = mr_run(c, model);
   if (rc) return rc;

@@ -120,9 +120,11 @@ class Engine:
                                         keys.ctypes.data_as(ctypes.c_void_p)), "mr_copy_topk")
         return songs, scores, keys
 
-    def copy_topk_device(self, songs_ptr: int, keys_ptr: int) -> None:
-        """Copy the last run's top-k lists into device buffers (D2D, synchronous)."""
-        _lib.check(self._L.mr_copy_topk_device(self._h, songs_ptr, keys_ptr), "mr_copy_topk_device")
+    def copy_topk_device(self, songs_ptr: int, keys_ptr: int, wait: bool = True) -> None:
+        """Copy the last run's top-k lists into device buffers (D2D); wait=False
+        only enqueues the copies on the engine stream."""
+        fn = self._L.mr_copy_topk_device if wait else self._L.mr_copy_topk_device_async
+        _lib.check(fn(self._h, songs_ptr, keys_ptr), "mr_copy_topk_device")
 
     def score_dense(self, model: Union[str, int]) -> np.ndarray:
         self.run(model)
@@ -134,11 +136,16 @@ class Engine:
         return tuple(p.value or 0 for p in ptrs)
 
     def merge_topk_device(self, n_shards: int, songs_ptr: int, keys_ptr: int, out_songs_ptr: int,
-                          out_keys_ptr: int, out_scores_ptr: int = 0) -> None:
-        """Merge n_shards gathered [shard][n_test][k] device lists on this GPU."""
-        _lib.check(self._L.mr_topk_merge_device(self._h, n_shards, self.n_test, self.topk_k, songs_ptr, keys_ptr,
-                                                None, out_songs_ptr, out_keys_ptr, out_scores_ptr or None),
-                   "mr_topk_merge_device")
+                          out_keys_ptr: int, out_scores_ptr: int = 0, wait: bool = True) -> None:
+        """Merge n_shards gathered [shard][n_test][k] device lists on this GPU
+        (wait=False: enqueued on the engine stream only)."""
+        if wait:
+            rc = self._L.mr_topk_merge_device(self._h, n_shards, self.n_test, self.topk_k, songs_ptr, keys_ptr,
+                                              None, out_songs_ptr, out_keys_ptr, out_scores_ptr or None)
+        else:
+            rc = self._L.mr_topk_merge_device_async(self._h, n_shards, self.n_test, self.topk_k, songs_ptr,
+                                                    keys_ptr, out_songs_ptr, out_keys_ptr, out_scores_ptr or None)
+        _lib.check(rc, "mr_topk_merge_device")
 
     # ---- device-resident models (combination models, evaluation) -------------
     def run_into(self, model: Union[str, int], dense_ptr: int) -> None:

@@ -1,6 +1,8 @@
 """Multi-GPU layouts: one process per GPU (torch.distributed over RCCL).
 
-Two partitions of the model's (test user, song) pairs, both exact:
+Partitions of the model's (test user, song) pairs, all exact (the 2-D
+ShardScorer combines the first two; include/mr_engine.h mr_group_* is the same
+layout inside the C ABI for single-process callers):
 
 * song-range shards (the north star; the reference's Spark "strategy 2",
   distributed.scala:477-479 ``parallelize(songs, 4)``): every rank holds the
@@ -77,48 +79,121 @@ def merge_gathered_host(g_songs, g_keys):
     return s, k
 
 
-class SongShardScorer:
-    """One rank of a song-sharded run: Engine on [lo, hi) + the top-k exchange."""
+def layout_2d(world: int, song_groups: Optional[int] = None) -> Tuple[int, int]:
+    """(G_s, G_u): song shards per user block and user blocks, G_s * G_u = world.
+    Rank r holds user block r // G_s and song shard r % G_s. song_groups=None:
+    all ranks shard songs (G_u = 1, the north star's layout)."""
+    gs = world if song_groups is None else int(song_groups)
+    if gs < 1 or world % gs:
+        raise ValueError(f"song_groups={gs} does not divide world={world}")
+    return gs, world // gs
 
-    def __init__(self, ds: Dataset, rank: int, world: int, device: int, *, topk: int = 10, dense: bool = True,
-                 out_dtype: str = "f32", time_kernels: bool = False,
-                 shards: Optional[List[Tuple[int, int]]] = None):
+
+def block_group(rank: int, world: int, song_groups: Optional[int] = None):
+    """The process group of the ranks sharing this rank's user block (the
+    all-gather of the exchange runs inside it). Every rank creates every
+    block's group (torch.distributed.new_group is collective). None = the
+    default group (one block)."""
+    import torch.distributed as dist
+
+    gs, gu = layout_2d(world, song_groups)
+    if gu == 1:
+        return None
+    mine = None
+    for b in range(gu):
+        g = dist.new_group(list(range(b * gs, (b + 1) * gs)))
+        if b == rank // gs:
+            mine = g
+    return mine
+
+
+class ShardScorer:
+    """One rank of a 2-D layout: test-user block b of G_u
+    (contiguous, sizes within one) x song-range shard g of G_s (Σ(c_tr + 1)
+    balanced). The ranks of a block exchange their per-user top-k lists with
+    ONE all-gather over RCCL (inside the block's process group) and merge them
+    on the device. G_u = 1 is the north star's song-shard layout (Spark strategy
+    2, distributed.scala:477-479), G_s = 1 the test-user blocks of strategy 1
+    (:468-470, no exchange); in between, stage 1 (replicated over the song
+    shards of a block) is split G_u ways.
+
+    No host synchronisation inside a step: the engine stream (run, list copy,
+    merge) and torch's stream (the all-gather) are ordered with events."""
+
+    def __init__(self, ds: Dataset, rank: int, world: int, device: int, *, song_groups: Optional[int] = None,
+                 topk: int = 10, dense: bool = True, out_dtype: str = "f32", time_kernels: bool = False,
+                 stage1: str = "auto"):
         import torch
         from .engine import Engine
 
-        self.shards = shards or song_shards(ds, world)
-        lo, hi = self.shards[rank]
+        self.gs, self.gu = layout_2d(world, song_groups)
         self.rank, self.world = rank, world
-        self.engine = Engine(ds, device=device, song_lo=lo, song_hi=hi, topk=topk, dense=dense,
-                             out_dtype=out_dtype, time_kernels=time_kernels)
+        self.block, self.shard = rank // self.gs, rank % self.gs
+        self.user_lo, self.user_hi = user_blocks(ds.n_test, self.gu)[self.block]
+        self.song_lo, self.song_hi = song_shards(ds, self.gs)[self.shard]
+        self.full = ds
+        self.ds = ds if self.gu == 1 else ds.subset_test_users(self.user_lo, self.user_hi)
+        self.group = block_group(rank, world, self.gs) if world > 1 else None
+        self.engine = Engine(self.ds, device=device, song_lo=self.song_lo, song_hi=self.song_hi, topk=topk,
+                             dense=dense, out_dtype=out_dtype, time_kernels=time_kernels, stage1=stage1)
         self.device = torch.device("cuda", device)
-        n_te = ds.n_test
+        n_te = self.ds.n_test
         self.local_songs = torch.empty((n_te, topk), dtype=torch.int32, device=self.device)
         self.local_keys = torch.empty((n_te, topk), dtype=torch.int64, device=self.device)
         self.out_songs = torch.empty((n_te, topk), dtype=torch.int32, device=self.device)
         self.out_keys = torch.empty((n_te, topk), dtype=torch.int64, device=self.device)
         self.out_scores = torch.empty((n_te, topk), dtype=torch.float64, device=self.device)
+        self.g_songs = torch.empty((self.gs * n_te, topk), dtype=torch.int32, device=self.device)
+        self.g_keys = torch.empty((self.gs * n_te, topk), dtype=torch.int64, device=self.device)
+        self._ext = torch.cuda.ExternalStream(self.engine.stream, device=self.device)
+
+    def pairs(self) -> int:
+        """Scored pairs of this rank: its users x its songs, minus the heard ones."""
+        te_off, te_songs = self.ds.te_off, self.ds.te_songs
+        heard = int(((te_songs >= self.song_lo) & (te_songs < self.song_hi)).sum())
+        return self.ds.n_test * (self.song_hi - self.song_lo) - heard
 
     def step(self, model: str) -> None:
-        """Score the shard, then exchange + merge top-k (ends synchronised)."""
+        """Score the (block, shard) cell, then exchange + merge the block's top-k
+        lists. Asynchronous: returns with the work queued on the streams."""
         import torch
+        import torch.distributed as dist
 
         e = self.engine
         e.run(model)
-        if self.world == 1:
+        if self.gs == 1:
             return
-        # D2D copy of the engine's lists into torch-owned send buffers; the
-        # engine call returns after its stream has drained.
+        e.copy_topk_device(self.local_songs.data_ptr(), self.local_keys.data_ptr(), wait=False)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self._ext)  # lists copied before the all-gather reads them
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self.g_songs, self.local_songs, group=self.group)
+            dist.all_gather_into_tensor(self.g_keys, self.local_keys, group=self.group)
+        else:  # gloo rehearsal with CUDA tensors: gather on the host
+            gs_, gk_ = exchange_topk(self.local_songs.cpu(), self.local_keys.cpu(), self.group)
+            self.g_songs.copy_(gs_.reshape(self.g_songs.shape))
+            self.g_keys.copy_(gk_.reshape(self.g_keys.shape))
+        self._ext.wait_stream(cur)  # the merge reads the gathered lists
+        e.merge_topk_device(self.gs, self.g_songs.data_ptr(), self.g_keys.data_ptr(), self.out_songs.data_ptr(),
+                            self.out_keys.data_ptr(), self.out_scores.data_ptr(), wait=False)
+
+    def sync(self) -> None:
+        import torch
+
+        self.engine.sync()
         torch.cuda.current_stream(self.device).synchronize()
-        e.copy_topk_device(self.local_songs.data_ptr(), self.local_keys.data_ptr())
-        g_songs, g_keys = exchange_topk(self.local_songs, self.local_keys)
-        torch.cuda.current_stream(self.device).synchronize()
-        e.merge_topk_device(self.world, g_songs.data_ptr(), g_keys.data_ptr(), self.out_songs.data_ptr(),
-                            self.out_keys.data_ptr(), self.out_scores.data_ptr())
 
     def topk(self):
-        """Merged (songs, keys) as numpy arrays (after step)."""
-        if self.world == 1:
+        """Merged (songs, keys) of this rank's user block, numpy (after step)."""
+        self.sync()
+        if self.gs == 1:
             s, _sc, k = self.engine.topk()
             return s, k
         return self.out_songs.cpu().numpy(), self.out_keys.cpu().numpy()
+
+
+class SongShardScorer(ShardScorer):
+    """The north star's layout: every rank a song shard of all test users."""
+
+    def __init__(self, ds: Dataset, rank: int, world: int, device: int, **kw):
+        super().__init__(ds, rank, world, device, song_groups=world, **kw)

@@ -129,6 +129,12 @@ def _worker(rank, world, port, layout, out):
         if layout == "songs":
             lo, hi = song_shards(ds, world)[rank]
             eng = _HostEngine(ds, dense, lo, hi)
+        elif layout == "2d":  # 2 user blocks x 2 song shards (sharding.ShardScorer's cells)
+            from musicrecommendation_amd.sharding import user_blocks
+
+            a, b = user_blocks(ds.n_test, 2)[rank // 2]
+            lo, hi = song_shards(ds, 2)[rank % 2]
+            eng = _HostEngine(ds.subset_test_users(a, b), dense[a:b], lo, hi)
         else:  # test-user blocks: each rank sees its users over all songs
             a, b = ds.n_test * rank // world, ds.n_test * (rank + 1) // world
             sub = ds.subset_test_users(a, b)
@@ -143,13 +149,13 @@ def _worker(rank, world, port, layout, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["songs", "users"])
+@pytest.mark.parametrize("layout", ["songs", "users", "2d"])
 def test_gloo_world2_threshold_map_reduction(layout):
-    world = 2
+    world = 4 if layout == "2d" else 2
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_worker, args=(world, _free_port(), layout, out), nprocs=world, join=True)
         res = dict(out)
     ds, z = synth_fixture("small")
     ref = evaluation.threshold_map(z["ibm"], ds)
-    assert res[0] == res[1] == ref
+    assert all(res[r] == ref for r in range(world))

@@ -66,3 +66,54 @@ def test_gloo_world2_song_shard_exchange(model):
     for r in range(world):
         assert np.array_equal(np.array(res[r][0]), ts)
         assert np.array_equal(np.array(res[r][1]), tk)
+
+
+def test_layout_2d():
+    from musicrecommendation_amd.sharding import layout_2d
+
+    assert layout_2d(8) == (8, 1)
+    assert layout_2d(8, 2) == (2, 4)
+    assert layout_2d(4, 4) == (4, 1)
+    with pytest.raises(ValueError):
+        layout_2d(6, 4)
+
+
+def _worker_2d(rank, world, port, song_groups, model, out):
+    """A rank of the 2-D layout with the oracle standing in for the engine:
+    its (user block, song shard) cell's top-k, the all-gather inside the
+    block's process group, the merge."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from musicrecommendation_amd.sharding import block_group, layout_2d
+
+        ds = synth.config("small").dataset()
+        gs, gu = layout_2d(world, song_groups)
+        grp = block_group(rank, world, song_groups)
+        a, b = user_blocks(ds.n_test, gu)[rank // gs]
+        lo, hi = song_shards(ds, gs)[rank % gs]
+        _, s, k = native.fp_model(ds, model, song_lo=lo, song_hi=hi, user_lo=a, user_hi=b, k=10, dense=False)
+        g_s, g_k = exchange_topk(torch.from_numpy(s), torch.from_numpy(k), grp)
+        assert g_s.shape[0] == gs
+        ms, mk = merge_gathered_host(g_s, g_k)
+        out[rank] = (a, b, ms.tolist(), mk.tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,song_groups", [(2, 1), (2, 2), (4, 2), (4, 4)])
+def test_gloo_2d_layout_exchange(world, song_groups):
+    model = "ibm"
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker_2d, args=(world, _free_port(), song_groups, model, out), nprocs=world, join=True)
+        res = dict(out)
+    ds = synth.config("small").dataset()
+    _, ts, tk = native.fp_model(ds, model, k=10, dense=False)
+    covered = np.zeros(ds.n_test, bool)
+    for r in range(world):
+        a, b, s, k = res[r]
+        assert np.array_equal(np.array(s), ts[a:b]) and np.array_equal(np.array(k), tk[a:b]), r
+        covered[a:b] = True
+    assert covered.all()
