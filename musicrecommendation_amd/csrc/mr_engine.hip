@@ -59,6 +59,7 @@ constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live 
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
 constexpr int kMaxTopkTile = 1024;        // songs per tile for the register top-k (4 per lane)
 constexpr int kMaxTopkLarge = 16;         // k limit of the wide-tile top-k (per-thread running lists)
+constexpr int kFusedPre = 4;              // fused shape: tile entries per thread prefetched before stage 1
 
 thread_local std::string g_err = "no error";
 
@@ -550,6 +551,8 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   long long tk = gk[NG];
   int tsg = gs[NG];
   if (tk < 0) { tk = 0; tsg = INT_MAX; }  // fewer than k valid row bests: every valid key
+  // (Compacting survivors per wave by ballot, one atomic per wave, measured
+  // slower: C2 14.30 vs 14.11 us per step, profiles/r02/c2_topk_ab.txt.)
 #pragma unroll 4
   for (int i = tid; i < n; i += NT) {
     long long key;
@@ -843,6 +846,7 @@ struct ScoreParams {
   const int* toff;               // tile-major train CSR: [n_tiles * n_tr + 1]; tile t, user v ->
                                  //   tsongs[toff[t*n_tr+v] .. toff[t*n_tr+v+1])
   const unsigned short* tsongs;  // tile-local song ids (s - tile start), rows sorted
+  const unsigned* tpack;         // fused shape: the same entries as (train user << 16) | tile-local song
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
   // fused stage 1 inputs
   const long long* trs_off;
@@ -909,22 +913,35 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
   const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
-  // Prefetch this thread's first epilogue scale (hidden behind stages 1-2).
-  const double sc0 = (MODEL == MR_IBM && tid < bw) ? p.sqrt_c[blo + tid] : 1.0;
+  // Prefetch this thread's epilogue scales (hidden behind stages 1-2): songs
+  // tid + 256 j of the tile, j < kFusedPre (the whole tile up to 1024 songs).
+  double sc[kFusedPre];
+#pragma unroll
+  for (int j = 0; j < kFusedPre; ++j) {
+    const int i = tid + j * kThreads;
+    sc[j] = (MODEL == MR_IBM && i < bw) ? p.sqrt_c[blo + i] : 1.0;
+  }
 
   if (FUSED) {
-    // The tile's row pointers do not depend on the test user: issue them now,
-    // they land while stage 1 runs (train users tid + 256 r, r < 4).
-    int pa[4], pb[4];
+    // Stage 2's inputs do not depend on the test user: the tile's entries
+    // (train user, song) are one contiguous run of tpack (tile-major CSR), so
+    // they are loaded now, coalesced, 4 per thread, and land while stage 1
+    // runs; stage 2 is then LDS work only (Y[v] lookups + atomics), balanced
+    // over the block whatever the segment lengths. (The per-neighbour segment
+    // walk it replaces waited on up to 3 dependent load batches for heavy
+    // listeners: 3.0 us median, 4.3 us max per C2 tile.)
+    const int e0 = p.toff[(size_t)tile * p.n_tr], e1 = p.toff[(size_t)(tile + 1) * p.n_tr];
+    unsigned pk[kFusedPre];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int j = 0; j < kFusedPre; ++j) {
+      const int i = e0 + tid + j * kThreads;
+      pk[j] = i < e1 ? p.tpack[i] : 0xffffffffu;
+    }
+    double str[kFusedPre];  // ubm: sqrt|S(v)| of this thread's first train users
+#pragma unroll
+    for (int r = 0; r < kFusedPre; ++r) {
       const int v = tid + r * kThreads;
-      pa[r] = pb[r] = 0;
-      if (v < p.n_tr) {
-        const int* bp = p.toff + (size_t)tile * p.n_tr + v;
-        pa[r] = bp[0];
-        pb[r] = bp[1];
-      }
+      str[r] = (MODEL == MR_UBM && v < p.n_tr) ? p.sqrt_tr[v] : 1.0;
     }
     unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
     for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
@@ -935,55 +952,34 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
                                  reinterpret_cast<int*>(smem_raw + L.s_pre),
                                  reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi);
     MR_STAMP(1);
-    const double rs_u = p.sqrt_te[u];
-    // 4 neighbours per thread in flight: row-pointer loads, then the first
-    // song of each segment, then the LDS atomics.
-    for (int v0 = tid; v0 < p.n_tr; v0 += 4 * kThreads) {
-      int a[4], b[4];
-      unsigned long long y[4];
+    if (MODEL == MR_UBM) {  // overlap counts -> fixed-point cosines (MR:142-148), in place
+      const double rs_u = p.sqrt_te[u];
+      for (int v = tid, r = 0; v < p.n_tr; v += kThreads, ++r) {
+        const unsigned long long y = Y[v];
+        if (y != 0ull) {
+          double sv;
+          if (r < kFusedPre) {  // static register index: no scratch spill
+            sv = str[0];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int v = v0 + r * kThreads;
-        y[r] = v < p.n_tr ? Y[v] : 0ull;
-        a[r] = b[r] = 0;
-        if (y[r] != 0ull) {
-          if (v0 == tid) {  // first pass: prefetched
-            a[r] = pa[r];
-            b[r] = pb[r];
+            for (int x = 1; x < kFusedPre; ++x) sv = r == x ? str[x] : sv;
           } else {
-            const int* bp = p.toff + (size_t)tile * p.n_tr + v;
-            a[r] = bp[0];
-            b[r] = bp[1];
+            sv = p.sqrt_tr[v];
           }
+          Y[v] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, sv, two_f);
         }
       }
-      // the first 4 songs of each of the 4 segments in one batch (16 loads in
-      // flight), then the atomics; longer segments continue 4 at a time
-      // (a song-at-a-time loop left heavy listeners' segments serialised on
-      // load latency).
-      int sg[4][4];
+      __syncthreads();
+    }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sg[r][e] = a[r] + e < b[r] ? (int)p.tsongs[a[r] + e] : -1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (sg[r][0] < 0) continue;
-        const int v = v0 + r * kThreads;
-        const unsigned long long q = (unsigned long long)neighbour_weight<MODEL>(
-            y[r], rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (sg[r][e] >= 0) atomicAdd(&acc[sg[r][e]], q);
-        for (int x = a[r] + 4; x < b[r]; x += 4) {
-          int t4[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) t4[e] = x + e < b[r] ? (int)p.tsongs[x + e] : -1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (t4[e] >= 0) atomicAdd(&acc[t4[e]], q);
-        }
-      }
+    for (int j = 0; j < kFusedPre; ++j) {
+      if (pk[j] == 0xffffffffu) continue;
+      const unsigned long long y = Y[pk[j] >> 16];
+      if (y != 0ull) atomicAdd(&acc[pk[j] & 0xffffu], y);
+    }
+    for (int i = e0 + tid + kFusedPre * kThreads; i < e1; i += kThreads) {  // tiles of > 1024 entries
+      const unsigned e = p.tpack[i];
+      const unsigned long long y = Y[e >> 16];
+      if (y != 0ull) atomicAdd(&acc[e & 0xffffu], y);
     }
   } else {
     __syncthreads();
@@ -1116,12 +1112,31 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   // Epilogue: scores -> dense row segment; keys stay in LDS for the top-k.
   const double inv_f = ldexp(1.0, -p.frac_bits);
   OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
-  for (int i = tid; i < bw; i += kThreads) {
+  // The thread's best (key desc, song asc) is tracked on the way (the
+  // threshold top-k starts from it; songs ascend per thread).
+  long long mk = kKeyNone;
+  int ms = INT_MAX;
+#pragma unroll
+  for (int j = 0; j < kFusedPre; ++j) {
+    const int i = tid + j * kThreads;
+    if (i < bw) {
+      const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+      double score = (double)(long long)acc[i] * inv_f;
+      if (MODEL == MR_IBM) score = score / sc[j];
+      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      const long long key = h ? kKeyNone : __double_as_longlong(score);
+      acc[i] = (unsigned long long)key;
+      if (key > mk) { mk = key; ms = blo + i; }
+    }
+  }
+  for (int i = tid + kFusedPre * kThreads; i < bw; i += kThreads) {  // tiles wider than 1024 songs
     const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
     double score = (double)(long long)acc[i] * inv_f;
-    if (MODEL == MR_IBM) score = score / (i == tid ? sc0 : p.sqrt_c[blo + i]);
+    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
     if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
-    acc[i] = h ? (unsigned long long)kKeyNone : (unsigned long long)__double_as_longlong(score);
+    const long long key = h ? kKeyNone : __double_as_longlong(score);
+    acc[i] = (unsigned long long)key;
+    if (key > mk) { mk = key; ms = blo + i; }
   }
   const int k = p.topk;
   if (k <= 0) return;
@@ -1136,11 +1151,13 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   };
   bool thr_done = false;  // threshold pass first (about k candidates, ranked in parallel)
   if (!p.topk_lists && k <= kThreads / 16) {
-    long long mk;
-    int ms;
-    thread_best<kThreads>(bw, get_key, mk, ms);
+#ifdef MR_STAMPS
+    long long* sbt = sb ? sb + 3 : nullptr;  // sub-phase stamps in slots 12-14
+#else
+    long long* sbt = nullptr;
+#endif
     thr_done = block_topk_threshold<kThreads, decltype(get_key), MR_TILE_ROWS>(
-        bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK, fk, fs);
+        bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK, fk, fs, sbt);
   }
   if (thr_done) {
   } else if (bs <= kMaxTopkTile) {
@@ -2154,6 +2171,7 @@ struct mr_ctx {
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
   DevBuf<int> te_songs, trs_users, toff, nbr_v, nbr_cnt, cand_song, top_song;
   DevBuf<unsigned short> tsongs;
+  DevBuf<unsigned> tpack;  // fused shape: tile entries as (train user << 16) | tile-local song
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
@@ -2179,7 +2197,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
+    tsongs.release(); tpack.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -2234,9 +2252,10 @@ int auto_block_songs(int width, int n_te, bool fused, int k, int n_tr) {
     return (int)std::max<long long>(256, std::min<long long>(kMaxBlockSongs, cover));
   const long long cap = k > 0 ? kMaxTopkTile : (fused ? 8192 : kMaxBlockSongs);
   // Fused: every tile repeats stage 1 and adds a candidate list to the
-  // user's merge, so aim for ~384 workgroups (C2: 33 tiles of 512 songs,
-  // 22.6 us vs 25.5 us at 256, scripts/c2_bs_sweep.py, profiles/r01_final).
-  const long long target = fused ? 384 : 1024;
+  // user's merge, so aim for ~256 workgroups (C2: 22 tiles of 768 songs,
+  // 14.5 us vs 15.2 at 512 and 14.7 at 1024 once stage 2 became LDS-only,
+  // scripts/c2_bs_sweep.py, profiles/r02).
+  const long long target = fused ? 256 : 1024;
   long long want = ((long long)width * std::max(1, n_te) + target - 1) / target;
   long long bs = ((want + 255) / 256) * 256;
   bs = std::max<long long>(256, std::min<long long>(cap, bs));
@@ -2584,6 +2603,14 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_upload(c->sbound, sb.data(), sb.size(), st))) return rc;
   }
   if ((rc = dev_upload(c->tsongs, tsongs.data(), tsongs.size(), st))) return rc;
+  if (fused) {  // n_tr <= 4096 and bs <= 8192: both halves fit 16 bits
+    std::vector<uint32_t> tpack(tsongs.size(), 0u);
+    for (size_t t = 0; t < (size_t)n_tiles; ++t)
+      for (int v = 0; v < n_tr; ++v)
+        for (int32_t i = toff[t * n_tr + v]; i < toff[t * n_tr + v + 1]; ++i)
+          tpack[i] = ((uint32_t)v << 16) | tsongs[i];
+    if ((rc = dev_upload(c->tpack, tpack.data(), tpack.size(), st))) return rc;
+  }
   if (pull) {
     if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
     if ((rc = dev_alloc(c->dbg, 1))) return rc;
@@ -2789,7 +2816,7 @@ int run_model(mr_ctx* c, int model) {
       sp.block_songs = c->block_songs; sp.n_tiles = c->n_tiles;
       sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
-      sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.sqrt_c = c->sqrt_c.p;
+      sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
       sp.trs_off = c->trs_off.p; sp.trs_users = c->trs_users.p; sp.q_song = c->q_song.p;
       sp.sqrt_tr = c->sqrt_tr.p; sp.sqrt_te = c->sqrt_te.p;
       sp.cap = c->cap;

@@ -48,6 +48,11 @@ phase("stage1", 0, 1)
 phase("stage2", 1, 2)
 phase("epilogue", 2, 3)
 phase("tile-topk", 3, 4)
+if (full[:, 12] != 0).all():  # diagnostic sub-phases of the fused tile top-k
+    phase("  topk best+rows", 3, 12)
+    phase("  topk row rank/tau", 12, 13)
+    phase("  topk collect", 13, 14)
+    phase("  topk rank+write", 14, 4)
 phase("handoff", 4, 5)
 phase("merge stage", 5, 6, last)
 phase("merge tournament", 6, 8, last)
