@@ -59,7 +59,8 @@ constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live 
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
 constexpr int kMaxTopkTile = 1024;        // songs per tile for the register top-k (4 per lane)
 constexpr int kMaxTopkLarge = 16;         // k limit of the wide-tile top-k (per-thread running lists)
-constexpr int kFusedPre = 4;              // fused shape: tile entries per thread prefetched before stage 1
+constexpr int kFusedPre = 4;
+constexpr int kWideMapDefault = 1;        // wide-shape block mapping (wide_map_opt)              // fused shape: tile entries per thread prefetched before stage 1
 
 thread_local std::string g_err = "no error";
 
@@ -1366,11 +1367,24 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   int* cpre = reinterpret_cast<int*>(smem_raw + L.cpre);
   int* s_scan = reinterpret_cast<int*>(smem_raw + L.s_scan);
 
-  // all tiles of a user on one XCD (round-robin dealing, speed only)
+  // Block -> (user, tile), speed only (blocks are dealt round-robin over the
+  // 8 XCDs): xcd_remap 1 = all tiles of a user on one XCD (the user's
+  // neighbour list is fetched into one L2); 2 = the (tile, user) pairs in
+  // tile-major order cut into 8 contiguous ranges, one per XCD, so the CUs of
+  // an XCD sweep the SAME tile's train-side rows (toff, tsongs: read almost
+  // whole by every user) for consecutive users at once and share them in L2.
   const int lin = blockIdx.y * gridDim.x + blockIdx.x;
   const int slot = lin >> 3;
-  const int bu = (slot / p.n_tiles) * 8 + (lin & 7);
-  const int tile = slot % p.n_tiles;
+  int bu, tile;
+  if (p.xcd_remap == 2) {
+    const int per_xcd = (gridDim.x * gridDim.y) >> 3;  // gridDim.y padded to a multiple of 8
+    const int pidx = (lin & 7) * per_xcd + slot;
+    tile = pidx / gridDim.y;
+    bu = pidx - tile * gridDim.y;
+  } else {
+    bu = (slot / p.n_tiles) * 8 + (lin & 7);
+    tile = slot % p.n_tiles;
+  }
   if (bu >= p.n_users) return;  // grid padded to a multiple of 8 users
   const int u = p.user0 + bu;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -2241,6 +2255,16 @@ int merge_rows_opt() {
   return rows;
 }
 
+// Wide-shape block mapping (ScoreParams.xcd_remap): 1 = tiles of a user on
+// one XCD, 2 = one tile's users per XCD; MR_WIDE_MAP=1/2 overrides.
+int wide_map_opt() {
+  static const int m = [] {
+    const char* e = std::getenv("MR_WIDE_MAP");
+    return e && std::atoi(e) == 1 ? 1 : (e && std::atoi(e) == 2 ? 2 : kWideMapDefault);
+  }();
+  return m;
+}
+
 int auto_block_songs(int width, int n_te, bool fused, int k, int n_tr) {
   // Separate: aim for >= ~1024 workgroups, tiles of 256..16384 songs; with top-k a tile
   // is at most kMaxTopkTile songs (4 candidates per lane in registers); the
@@ -2804,7 +2828,8 @@ int run_model(mr_ctx* c, int model) {
       const int ny = std::min(65528, nb - y0);
       // separate shape: all tiles of a user on one XCD (grid padded to 8 users)
       const bool wide = c->shape == kShapeWide;
-      const int remap = (c->shape == kShapeSeparate && c->n_tiles > 1) || wide;
+      int remap = (c->shape == kShapeSeparate && c->n_tiles > 1) || wide;
+      if (wide) remap = wide_map_opt();
       const int gy = remap ? (ny + 7) / 8 * 8 : ny;
       ScoreParams sp{};
       sp.chunk = c->chunk; sp.n_chunks = c->n_chunks;
