@@ -673,12 +673,23 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
                                                 const long long* q_song, long long* s_lo, long long* s_w,
                                                 int* s_pre, int* s_scan, Add add, Mark mark, bool ranged = false,
                                                 int v0 = 0, int v1 = 0, const int* sbound = nullptr,
-                                                int chunk_idx = 0, int nc1 = 0) {
+                                                int chunk_idx = 0, int nc1 = 0, const int2* te_rng = nullptr,
+                                                const long long* te_q = nullptr) {
   const int tid = threadIdx.x;
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
     int len = 0;
-    if (tid < n) {
+    if (tid < n && te_rng && !ranged) {
+      // listener range and weight of each song of T(u) resolved at load time
+      // (mr_load: the songsToUsersMap lookup of MR:232 per test-visible song):
+      // loaded beside te_songs, one dependent level fewer
+      const int s2 = te_songs[base + tid];
+      const int2 r = te_rng[base + tid];
+      len = r.y;
+      s_lo[tid] = r.x;
+      s_w[tid] = (MODEL == MR_IBM) ? te_q[base + tid] : 1ll;
+      mark(s2);
+    } else if (tid < n) {
       const int s2 = te_songs[base + tid];
       long long lo = trs_off[s2], hi = trs_off[s2 + 1];
       if (ranged && sbound) {  // precomputed chunk boundaries of L_tr(s2) (mr_load)
@@ -753,14 +764,15 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
                                                       long long* s_lo, long long* s_w, int* s_pre, int* s_scan,
                                                       unsigned* heard, int blo, int bhi, bool ranged = false,
                                                       int v0 = 0, int v1 = 0, const int* sbound = nullptr,
-                                                      int chunk_idx = 0, int nc1 = 0) {
+                                                      int chunk_idx = 0, int nc1 = 0, const int2* te_rng = nullptr,
+                                                      const long long* te_q = nullptr) {
   walk_neighbours<MODEL>(
       t0, t1, te_songs, trs_off, trs_users, q_song, s_lo, s_w, s_pre, s_scan,
       [&](int v, unsigned long long w) { atomicAdd(&Y[v - v0], w); },
       [&](int s2) {
         if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
       },
-      ranged, v0, v1, sbound, chunk_idx, nc1);
+      ranged, v0, v1, sbound, chunk_idx, nc1, te_rng, te_q);
 }
 
 // Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
@@ -848,6 +860,8 @@ struct ScoreParams {
                                  //   tsongs[toff[t*n_tr+v] .. toff[t*n_tr+v+1])
   const unsigned short* tsongs;  // tile-local song ids (s - tile start), rows sorted
   const unsigned* tpack;         // fused shape: the same entries as (train user << 16) | tile-local song
+  const int2* te_rng;            // fused shape: per te_songs entry, (trs_off[s2], c_tr(s2))
+  const long long* te_q;         // fused shape: per te_songs entry, q_song[s2]
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
   // fused stage 1 inputs
   const long long* trs_off;
@@ -951,7 +965,8 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
                                  reinterpret_cast<long long*>(smem_raw + L.s_lo),
                                  reinterpret_cast<long long*>(smem_raw + L.s_w),
                                  reinterpret_cast<int*>(smem_raw + L.s_pre),
-                                 reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi);
+                                 reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi, false, 0, 0,
+                                 nullptr, 0, 0, p.te_rng, p.te_q);
     MR_STAMP(1);
     if (MODEL == MR_UBM) {  // overlap counts -> fixed-point cosines (MR:142-148), in place
       const double rs_u = p.sqrt_te[u];
@@ -1579,15 +1594,17 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 // int64 accumulators + the train users' weights fit the 160 KiB LDS, e.g. the
 // C2 subset: 16770 songs x 500 train users). MR:140-166 / MR:230-257.
 // ---------------------------------------------------------------------------
-constexpr int kUserRound = 512;  // train users staged per stage-2 round
 constexpr int kUserMaxPerThread = 20;  // songs per thread: 20 x 1024 x 8 B = the whole LDS
+constexpr int kUserPre = 28;           // (train user, song) entries per thread prefetched before stage 1
 // Not chosen automatically: at C2 (10 test users) one workgroup per user
-// leaves 246 CUs idle and its three dependent gathers are latency-bound
-// (31.7 us vs 26.6 us fused); scripts/shape_sweep.py has the other sizes.
+// leaves 246 CUs idle and serialises a whole row's epilogue and top-k on one
+// CU: 21.2 us vs 14.0 us fused after its stage 2 became LDS-only (31.7 us in
+// round 1; profiles/r02/c2_bs_sweep_user_v2.txt, phase_stamps_c2_user_v2.txt:
+// stage 1 8.4, stage 2 2.6, epilogue 5.6, top-k 4.0 us).
 constexpr bool kUserAuto = false;
 template <int NT>
 struct UserLds {
-  int acc, heard, y, st_a, st_pre, st_q, s_scan, wk, ws, fk, fs, gm, total;
+  int acc, heard, y, s_scan, wk, ws, fk, fs, gm, total;
 };
 template <int NT>
 __host__ __device__ inline UserLds<NT> user_lds(int bs, int n_tr, int k) {
@@ -1599,9 +1616,6 @@ __host__ __device__ inline UserLds<NT> user_lds(int bs, int n_tr, int k) {
   L.acc = o; o = align16(o + (bs * 8 > s1 ? bs * 8 : s1));
   L.heard = o; o = align16(o + ((bs + 31) / 32) * 4);
   L.y = o; o = align16(o + (n_tr > 0 ? n_tr : 1) * 8);
-  L.st_a = o; o = align16(o + kUserRound * 4);
-  L.st_pre = o; o = align16(o + (kUserRound + 1) * 4);
-  L.st_q = o; o = align16(o + kUserRound * 8);
   L.s_scan = o; o = align16(o + NW * 4);
   L.wk = o; o = align16(o + NW * kk * 8);
   L.ws = o; o = align16(o + NW * kk * 4);
@@ -1635,6 +1649,15 @@ __global__ __launch_bounds__(kWideThreads) void k_score_user(ScoreParams p) {
     const int i = tid + j * NT;
     sc[j] = (MODEL == MR_IBM && i < bw) ? p.sqrt_c[blo + i] : 1.0;
   }
+  // stage 2's input, independent of the test user: the shard's (train user,
+  // song) entries (tpack, one contiguous coalesced run), kUserPre per thread
+  const int e1 = p.toff[p.n_tr];
+  unsigned pk[kUserPre];
+#pragma unroll
+  for (int j = 0; j < kUserPre; ++j) {
+    const int i = tid + j * NT;
+    pk[j] = i < e1 ? p.tpack[i] : 0xffffffffu;
+  }
 
   for (int i = tid; i < p.n_tr; i += NT) Y[i] = 0ull;
   for (int i = tid; i < (bw + 31) / 32; i += NT) heard[i] = 0u;
@@ -1652,10 +1675,17 @@ __global__ __launch_bounds__(kWideThreads) void k_score_user(ScoreParams p) {
       int len = 0;
       if (tid < n) {
         const int s2 = p.te_songs[base + tid];
-        const long long lo = p.trs_off[s2], hi = p.trs_off[s2 + 1];
-        len = (int)(hi - lo);
-        s_lo[tid] = lo;
-        s_w[tid] = MODEL == MR_IBM ? p.q_song[s2] : 1ll;
+        if (p.te_rng) {  // listener range resolved at load time
+          const int2 r = p.te_rng[base + tid];
+          len = r.y;
+          s_lo[tid] = r.x;
+          s_w[tid] = MODEL == MR_IBM ? p.te_q[base + tid] : 1ll;
+        } else {
+          const long long lo = p.trs_off[s2], hi = p.trs_off[s2 + 1];
+          len = (int)(hi - lo);
+          s_lo[tid] = lo;
+          s_w[tid] = MODEL == MR_IBM ? p.q_song[s2] : 1ll;
+        }
         if (s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
       }
       int total;
@@ -1692,60 +1722,29 @@ __global__ __launch_bounds__(kWideThreads) void k_score_user(ScoreParams p) {
   __syncthreads();
   MR_STAMP(1);
 
-  // stage 2: rounds of kUserRound train users; their segment lengths are
-  // scanned so the entries spread evenly over the workgroup (segments are
-  // whole histories here, heavy-tailed).
-  {
-    int* st_a = reinterpret_cast<int*>(smem_raw + L.st_a);
-    int* st_pre = reinterpret_cast<int*>(smem_raw + L.st_pre);
-    unsigned long long* st_q = reinterpret_cast<unsigned long long*>(smem_raw + L.st_q);
+  // stage 2: LDS only — every prefetched (train user, song) entry whose user
+  // is a neighbour adds its weight; UBM first turns the overlap counts into
+  // fixed-point cosines in place (MR:142-148).
+  if (MODEL == MR_UBM) {
     const double rs_u = p.sqrt_te[u];
-    for (int r0 = 0; r0 < p.n_tr; r0 += kUserRound) {
-      int len = 0;
-      if (tid < kUserRound) {
-        const int v = r0 + tid;
-        int a = 0;
-        if (v < p.n_tr) {
-          const unsigned long long y = Y[v];
-          if (y != 0ull) {
-            a = p.toff[v];
-            len = p.toff[v + 1] - a;
-            st_q[tid] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0,
-                                                                    two_f);
-          }
-        }
-        st_a[tid] = a;
-      }
-      int total;
-      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
-      if (tid < kUserRound) st_pre[tid] = pre;
-      __syncthreads();
-      constexpr int E = 16;
-      for (int j0 = tid; j0 < total; j0 += E * NT) {
-        int song[E], it[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int j = j0 + e * NT;
-          song[e] = -1;
-          it[e] = 0;
-          if (j < total) {
-            int lo = 0, hi = kUserRound;  // last item with st_pre[item] <= j
-#pragma unroll
-            for (int st = 0; st < 9; ++st) {
-              const int m = (lo + hi) >> 1;
-              if (st_pre[m] <= j) lo = m; else hi = m;
-            }
-            song[e] = (int)p.tsongs[st_a[lo] + (j - st_pre[lo])];
-            it[e] = lo;
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e)
-          if (song[e] >= 0) atomicAdd(&acc[song[e]], st_q[it[e]]);
-      }
-      __syncthreads();
+    for (int v = tid; v < p.n_tr; v += NT) {
+      const unsigned long long y = Y[v];
+      if (y != 0ull) Y[v] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, p.sqrt_tr[v], two_f);
     }
+    __syncthreads();
   }
+#pragma unroll
+  for (int j = 0; j < kUserPre; ++j) {
+    if (pk[j] == 0xffffffffu) continue;
+    const unsigned long long y = Y[pk[j] >> 16];
+    if (y != 0ull) atomicAdd(&acc[pk[j] & 0xffffu], y);
+  }
+  for (int i = tid + kUserPre * NT; i < e1; i += NT) {  // shards of more entries
+    const unsigned e = p.tpack[i];
+    const unsigned long long y = Y[e >> 16];
+    if (y != 0ull) atomicAdd(&acc[e & 0xffffu], y);
+  }
+  __syncthreads();
   MR_STAMP(2);
 
   // epilogue: scores -> dense row; keys back into acc (scale loads batched)
@@ -2186,6 +2185,8 @@ struct mr_ctx {
   DevBuf<int> te_songs, trs_users, toff, nbr_v, nbr_cnt, cand_song, top_song;
   DevBuf<unsigned short> tsongs;
   DevBuf<unsigned> tpack;  // fused shape: tile entries as (train user << 16) | tile-local song
+  DevBuf<int2> te_rng;     // fused shape: listener range of every test-visible song
+  DevBuf<long long> te_q;  // fused shape: its ibm weight q_song
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
@@ -2211,7 +2212,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); tpack.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
+    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -2627,13 +2628,25 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_upload(c->sbound, sb.data(), sb.size(), st))) return rc;
   }
   if ((rc = dev_upload(c->tsongs, tsongs.data(), tsongs.size(), st))) return rc;
-  if (fused) {  // n_tr <= 4096 and bs <= 8192: both halves fit 16 bits
+  if (fused || user) {  // n_tr <= 4096 and bs <= 65536: both halves fit 16 bits
     std::vector<uint32_t> tpack(tsongs.size(), 0u);
     for (size_t t = 0; t < (size_t)n_tiles; ++t)
       for (int v = 0; v < n_tr; ++v)
         for (int32_t i = toff[t * n_tr + v]; i < toff[t * n_tr + v + 1]; ++i)
           tpack[i] = ((uint32_t)v << 16) | tsongs[i];
     if ((rc = dev_upload(c->tpack, tpack.data(), tpack.size(), st))) return rc;
+    // The songsToUsersMap lookup (MR:232) of every test-visible song, resolved
+    // once: its listener range in trs_users and its ibm weight.
+    const size_t nte = (size_t)d->te_off[n_te];
+    std::vector<int2> rng(std::max<size_t>(1, nte));
+    std::vector<long long> tq(std::max<size_t>(1, nte));
+    for (size_t i = 0; i < nte; ++i) {
+      const int s2 = d->te_songs[i];
+      rng[i] = make_int2((int)trs_off[s2], (int)(trs_off[s2 + 1] - trs_off[s2]));
+      tq[i] = q_song[s2];
+    }
+    if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
+    if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
   }
   if (pull) {
     if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
@@ -2842,6 +2855,10 @@ int run_model(mr_ctx* c, int model) {
       sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
+      sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused / user shapes (else null)
+#ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
+      sp.te_rng = nullptr;
+#endif
       sp.trs_off = c->trs_off.p; sp.trs_users = c->trs_users.p; sp.q_song = c->q_song.p;
       sp.sqrt_tr = c->sqrt_tr.p; sp.sqrt_te = c->sqrt_te.p;
       sp.cap = c->cap;
