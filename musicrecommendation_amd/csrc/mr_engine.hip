@@ -1360,13 +1360,17 @@ __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
 
 constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_R
-#define MR_WIDE_R 4         // neighbours per thread per iteration (wide kernel; 2/4/8 within 3%)
+#define MR_WIDE_R 2         // neighbours per thread per iteration (wide kernel; with the pipeline below
+                            // 2 beats 4 by 2 % at C4, profiles/r02/c4/pipeline_ab.txt)
 #endif
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
 #ifndef MR_WIDE_PREFETCH
 #define MR_WIDE_PREFETCH 0  // 1 = load the next iteration's list entries ahead
+#endif
+#ifndef MR_WIDE_PIPE
+#define MR_WIDE_PIPE 1      // 1 = 3-level software pipeline (list i+2, toff i+1, songs i)
 #endif
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
@@ -1451,6 +1455,52 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     };
+#if MR_WIDE_PIPE
+    // Software pipeline over iterations: iteration i gathers its segments
+    // while the toff pairs of i+1 and the list entries of i+2 are in flight
+    // (one memory latency covers the three dependent levels).
+    auto load_offs = [&](const int (&v)[R], int (&a)[R], int (&b)[R]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a[r] = b[r] = 0;
+        if (v[r] >= 0) { a[r] = toff_t[v[r]]; b[r] = toff_t[v[r] + 1]; }
+      }
+    };
+    int v0[R], a0[R], b0[R], v1[R], a1[R], b1[R], v2[R];
+    unsigned long long q0[R], q1[R], q2[R];
+    load_list(tid, v0, q0);
+    load_offs(v0, a0, b0);
+    load_list(tid + R * NT, v1, q1);
+    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
+      int sg[R][kSeg];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) sg[r][j] = a0[r] + j < b0[r] ? (int)p.tsongs[a0[r] + j] : -1;
+      load_offs(v1, a1, b1);                 // iteration i+1
+      load_list(k0 + 2 * R * NT, v2, q2);    // iteration i+2
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j)
+          if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q0[r]);
+        for (int x0 = a0[r] + kSeg; x0 < b0[r]; x0 += kSeg) {
+          int st[kSeg];
+#pragma unroll
+          for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b0[r] ? (int)p.tsongs[x0 + j] : -1;
+#pragma unroll
+          for (int j = 0; j < kSeg; ++j)
+            if (st[j] >= 0) atomicAdd(&acc[st[j]], q0[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a0[r] = a1[r]; b0[r] = b1[r]; q0[r] = q1[r];
+        v1[r] = v2[r]; q1[r] = q2[r];
+      }
+    }
+    (void)v0;
+#else
 #if MR_WIDE_PREFETCH
     int vn[R];
     unsigned long long qn[R];
@@ -1495,6 +1545,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     }
+#endif
   }
   __syncthreads();
   MR_STAMP(2);
