@@ -726,8 +726,34 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
 #pragma unroll
       for (int r = 0; r < 16; ++r) { v[r] = -1; wv[r] = 0ull; }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (ib + g * 4 * kThreads >= total) break;
+      for (int g2 = 0; g2 < 4; g2 += 2) {  // two groups of 4 at a time
+        if (ib + g2 * 4 * kThreads >= total) break;
+        if (ib + (g2 + 1) * 4 * kThreads < total) {
+          // both groups hold entries (heavy users): 8 searches in lockstep, so
+          // the second group's LDS reads overlap the first's (C2's heaviest
+          // user: stage 1 4.9 -> 4.5 us)
+          int a[8], b[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { a[e] = 0; b[e] = n; }
+          for (int st = 0; st < nsteps; ++st) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int i = i0 + (g2 * 4 + e) * kThreads;
+              const int m = (a[e] + b[e]) >> 1;
+              if (s_pre[m] <= i) a[e] = m; else b[e] = m;
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int i = i0 + (g2 * 4 + e) * kThreads;
+            if (i < total) {
+              v[g2 * 4 + e] = trs_users[s_lo[a[e]] + (i - s_pre[a[e]])];
+              wv[g2 * 4 + e] = (unsigned long long)s_w[a[e]];
+            }
+          }
+          continue;
+        }
+        const int g = g2;  // one group of 4
         int a[4], b[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) { a[e] = 0; b[e] = n; }
