@@ -500,6 +500,47 @@ __device__ __forceinline__ void thread_best(int n, Get get, long long& mk, int& 
     if (key >= 0) take_if_before(mk, ms, key, song);
   }
 }
+// Ranks of nc <= 256 survivor candidates ck/cs among themselves (total order
+// (key desc, song asc)): rank < k -> output slot; slots past nc get (-1, -1).
+// crank: 256 zeroed ints. All threads call it; it ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void rank_survivors(int nc, int k, const long long* ck, const int* cs, int* crank,
+                                               long long* out_k, int* out_s) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (nc * nc > 16 * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
+    if (tid < 64) {
+      long long rk[4];
+      int rs[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = lane + 64 * j;
+        rk[j] = c < nc ? ck[c] : kKeyNone;
+        rs[j] = c < nc ? cs[c] : INT_MAX;
+      }
+      wave_topk_regs<4>(rk, rs, k, out_k, out_s);
+    }
+    __syncthreads();
+    return;
+  }
+  if (nc > 0) {  // candidate ranks: nc x nc comparisons, <= 16 per thread
+    const int sl = NT / nc;  // slices per candidate (nc <= 256 <= NT)
+    const int per = (nc + sl - 1) / sl;
+    if (tid < sl * nc) {
+      const int i = tid % nc, j0 = (tid / nc) * per;
+      const long long mine = ck[i];
+      const int mines = cs[i];
+      int c = 0;
+      for (int j = j0; j < min(nc, j0 + per); ++j) c += cand_before(ck[j], cs[j], mine, mines) ? 1 : 0;
+      if (c) atomicAdd(&crank[i], c);
+    }
+  }
+  __syncthreads();
+  if (tid < nc && crank[tid] < k) { out_k[crank[tid]] = ck[tid]; out_s[crank[tid]] = cs[tid]; }
+  if (tid >= nc && tid < k) { out_k[tid] = kKeyNone; out_s[tid] = -1; }  // fewer than k entries
+  __syncthreads();
+}
+
+
 // NG rows of NT / NG threads: more rows give a tighter tau (fewer survivors
 // to rank) for NG^2 / NT comparisons per thread.
 template <int NT, typename Get, int NG = NT / 16>
@@ -568,37 +609,7 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   stamp_at(sb, 11);
   const int nc = *counter;
   if (nc > cap) return false;
-  if (nc * nc > 16 * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
-    if (tid < 64) {
-      long long rk[4];
-      int rs[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = lane + 64 * j;
-        rk[j] = c < nc ? ck[c] : kKeyNone;
-        rs[j] = c < nc ? cs[c] : INT_MAX;
-      }
-      wave_topk_regs<4>(rk, rs, k, out_k, out_s);
-    }
-    __syncthreads();
-    return true;
-  }
-  if (nc > 0) {  // candidate ranks: nc x nc comparisons, <= 16 per thread
-    const int sl = NT / nc;  // slices per candidate (nc <= 256 <= NT)
-    const int per = (nc + sl - 1) / sl;
-    if (tid < sl * nc) {
-      const int i = tid % nc, j0 = (tid / nc) * per;
-      const long long mine = ck[i];
-      const int mines = cs[i];
-      int c = 0;
-      for (int j = j0; j < min(nc, j0 + per); ++j) c += cand_before(ck[j], cs[j], mine, mines) ? 1 : 0;
-      if (c) atomicAdd(&crank[i], c);
-    }
-  }
-  __syncthreads();
-  if (tid < nc && crank[tid] < k) { out_k[crank[tid]] = ck[tid]; out_s[crank[tid]] = cs[tid]; }
-  if (tid >= nc && tid < k) { out_k[tid] = kKeyNone; out_s[tid] = -1; }  // fewer than k entries
-  __syncthreads();
+  rank_survivors<NT>(nc, k, ck, cs, crank, out_k, out_s);
   return true;
 }
 
@@ -1294,6 +1305,9 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       __syncthreads();
       MR_STAMP(6);
       bool merged = false;
+      // (A threshold on the sorted lists' HEADS — the k-th best head — measured
+      // 16.7 vs 14.0 us per C2 step: it is a much looser bound than the row
+      // bests, ~5x the survivors to rank; profiles/r02/c2_merge_heads_ab.txt.)
       if (!p.topk_lists && done == 0 && nl == p.n_tiles && k <= kThreads / 16) {  // one pass: threshold select
         auto get_c = [&](int i, long long& key, int& song) { key = mk[i]; song = ms[i]; };
         long long bk;
