@@ -1400,18 +1400,14 @@ __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
 
 constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_R
-#define MR_WIDE_R 2         // neighbours per thread per iteration (wide kernel; with the pipeline below
-                            // 2 beats 4 by 2 % at C4, profiles/r02/c4/pipeline_ab.txt)
+#define MR_WIDE_R 2         // neighbours per thread per iteration (wide kernel; with the 3-level software
+                            // pipeline 2 beats 4 by 2 % at C4 and a next-list-only prefetch loses,
+                            // profiles/r02/c4/pipeline_ab.txt)
 #endif
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
-#ifndef MR_WIDE_PREFETCH
-#define MR_WIDE_PREFETCH 0  // 1 = load the next iteration's list entries ahead
-#endif
-#ifndef MR_WIDE_PIPE
-#define MR_WIDE_PIPE 1      // 1 = 3-level software pipeline (list i+2, toff i+1, songs i)
-#endif
+
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
@@ -1495,7 +1491,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     };
-#if MR_WIDE_PIPE
     // Software pipeline over iterations: iteration i gathers its segments
     // while the toff pairs of i+1 and the list entries of i+2 are in flight
     // (one memory latency covers the three dependent levels).
@@ -1540,52 +1535,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       }
     }
     (void)v0;
-#else
-#if MR_WIDE_PREFETCH
-    int vn[R];
-    unsigned long long qn[R];
-    load_list(tid, vn, qn);
-#endif
-    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
-      int v[R], a[R], b[R];
-      unsigned long long q[R];
-#if MR_WIDE_PREFETCH
-#pragma unroll
-      for (int r = 0; r < R; ++r) { v[r] = vn[r]; q[r] = qn[r]; }
-      load_list(k0 + R * NT, vn, qn);  // next iteration's entries, in flight during this one
-#else
-      load_list(k0, v, q);
-#endif
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        a[r] = b[r] = 0;
-        if (v[r] >= 0) {
-          a[r] = toff_t[v[r]];
-          b[r] = toff_t[v[r] + 1];
-        }
-      }
-      int sg[R][kSeg];
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j) sg[r][j] = a[r] + j < b[r] ? (int)p.tsongs[a[r] + j] : -1;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j)
-          if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q[r]);
-        // long segments (heavy listeners): kSeg independent loads per batch
-        for (int x0 = a[r] + kSeg; x0 < b[r]; x0 += kSeg) {
-          int st[kSeg];
-#pragma unroll
-          for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b[r] ? (int)p.tsongs[x0 + j] : -1;
-#pragma unroll
-          for (int j = 0; j < kSeg; ++j)
-            if (st[j] >= 0) atomicAdd(&acc[st[j]], q[r]);
-        }
-      }
-    }
-#endif
   }
   __syncthreads();
   MR_STAMP(2);

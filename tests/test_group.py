@@ -134,3 +134,50 @@ def test_group_errors():
         Group(ds, song_shards=ds.n_songs + 1)
     with pytest.raises(_lib.EngineError):
         Group(ds, user_blocks=ds.n_test + 1)
+
+
+@pytest.mark.gpu
+def test_c3_song_sharded_group_equals_one_context():
+    """C3 ("User+ItemBased 10k/1k, song-id sharded across 2 MI355X with RCCL
+    all-gather"): the same 2-shard layout through the group (device-copy
+    transport on the 1-GPU box), both models, top-10 and the dense model
+    gathered on the device, bitwise against one context."""
+    import torch
+    from musicrecommendation_amd.engine import Engine
+
+    ds = synth.config("c3").dataset()
+    with Engine(ds, out_dtype="f32", topk=10) as e:
+        ref = {}
+        for model in ("ubm", "ibm"):
+            e.run(model)
+            ref[model] = (e.dense(), e.topk()[0], e.topk()[2])
+    with Group(ds, song_shards=2, out_dtype="f32", topk=10) as g:
+        assert [(lo, hi) for lo, hi, *_ in g.layout] == song_shards(ds, 2)
+        for model in ("ubm", "ibm"):
+            g.run(model)
+            songs, _scores, keys = g.topk()
+            d_ref, s_ref, k_ref = ref[model]
+            assert np.array_equal(songs, s_ref) and np.array_equal(keys, k_ref), model
+            bufs = [torch.empty((ds.n_test, ds.n_songs), dtype=torch.float32, device="cuda") for _ in range(2)]
+            torch.cuda.synchronize()
+            g.allgather_dense([b.data_ptr() for b in bufs])
+            for b in bufs:
+                assert np.array_equal(b.cpu().numpy(), d_ref, equal_nan=True), model
+            del bufs
+
+
+@pytest.mark.gpu
+def test_group_uneven_blocks_and_topk_only():
+    from musicrecommendation_amd.engine import Engine
+
+    ds = synth.config("c2", n_test=23).dataset()  # 23 users over 3 blocks: 7 / 8 / 8
+    with Engine(ds, out_dtype="f64", topk=16, dense=False) as e:
+        e.run("ubm")
+        s_ref, _sc, k_ref = e.topk()
+    with Group(ds, song_shards=2, user_blocks=3, out_dtype="f64", topk=16, dense=False) as g:
+        assert [(ulo, uhi) for _slo, _shi, ulo, uhi, _d in g.layout[::2]] == [(0, 7), (7, 15), (15, 23)]
+        g.run("ubm")
+        s, _sc, k = g.topk()
+        assert np.array_equal(s, s_ref) and np.array_equal(k, k_ref)
+        with pytest.raises(_lib.EngineError):
+            g.dense()  # dense=0
