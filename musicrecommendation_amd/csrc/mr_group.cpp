@@ -229,17 +229,25 @@ int run_group(mr_group* G, int model) {
   if (rc_mode) {
     Rccl& R = rccl();
     G_NCCL(R.group_start());
-    for (auto& x : G->m) {
-      const size_t n = (size_t)(x.user_hi - x.user_lo) * k;
-      int32_t* ts;
-      int64_t* tk;
-      int rc = mr_device_outputs(x.ctx, nullptr, &ts, &tk, nullptr);
-      if (rc) { (void)R.group_end(); return rc; }
-      G_HIP(hipSetDevice(x.dev));
-      G_NCCL(R.all_gather(tk, x.gkey.p, n, ncclInt64, x.comm, x.stream));
-      G_NCCL(R.all_gather(ts, x.gsong.p, n, ncclInt32, x.comm, x.stream));
-    }
-    G_NCCL(R.group_end());
+    // Every call between ncclGroupStart and ncclGroupEnd; an error still
+    // closes the group (RCCL's group state is thread-global).
+    auto enqueue = [&]() -> int {
+      for (auto& x : G->m) {
+        const size_t n = (size_t)(x.user_hi - x.user_lo) * k;
+        int32_t* ts;
+        int64_t* tk;
+        int rc = mr_device_outputs(x.ctx, nullptr, &ts, &tk, nullptr);
+        if (rc) return rc;
+        G_HIP(hipSetDevice(x.dev));
+        G_NCCL(R.all_gather(tk, x.gkey.p, n, ncclInt64, x.comm, x.stream));
+        G_NCCL(R.all_gather(ts, x.gsong.p, n, ncclInt32, x.comm, x.stream));
+      }
+      return MR_OK;
+    };
+    const int erc = enqueue();
+    const ncclResult_t end = R.group_end();
+    if (erc) return erc;
+    if (end != ncclSuccess) return gfail(MR_E_RCCL, "ncclGroupEnd: %s", R.error_string(end));
     for (auto& x : G->m) {
       const int rc = mr_internal::merge_async(x.ctx, gs, x.user_hi - x.user_lo, k, x.gsong.p,
                                               reinterpret_cast<const int64_t*>(x.gkey.p), x.msong.p,
@@ -610,11 +618,17 @@ int mr_group_allgather_dense(mr_group* g, void* const* dst) {
     Rccl& R = rccl();
     const ncclDataType_t t = g->opt.out_dtype == MR_OUT_F64 ? ncclFloat64 : ncclFloat32;
     G_NCCL(R.group_start());
-    for (auto& x : g->m) {
-      G_HIP(hipSetDevice(x.dev));
-      G_NCCL(R.all_gather(x.send.p, x.recv.p, (size_t)(x.user_hi - x.user_lo) * g->w_max, t, x.comm, x.stream));
-    }
-    G_NCCL(R.group_end());
+    auto enqueue = [&]() -> int {
+      for (auto& x : g->m) {
+        G_HIP(hipSetDevice(x.dev));
+        G_NCCL(R.all_gather(x.send.p, x.recv.p, (size_t)(x.user_hi - x.user_lo) * g->w_max, t, x.comm, x.stream));
+      }
+      return MR_OK;
+    };
+    const int erc = enqueue();
+    const ncclResult_t end = R.group_end();
+    if (erc) return erc;
+    if (end != ncclSuccess) return gfail(MR_E_RCCL, "ncclGroupEnd: %s", R.error_string(end));
     for (auto& x : g->m) {  // [G_s][n_bk][w_max] -> rows of n_songs
       const size_t nbk = (size_t)(x.user_hi - x.user_lo);
       G_HIP(hipSetDevice(x.dev));
