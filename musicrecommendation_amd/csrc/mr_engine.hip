@@ -885,10 +885,7 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
 // stage 2 (+ fused stage 1, + stage 3): one workgroup per (song tile, test
 // user). MR:159-166 (ubm rank), MR:249-257 (ibm rank), MR:105-111 (pairs).
 // ---------------------------------------------------------------------------
-constexpr int kKargUsers = 64;  // test users whose T(u) offsets travel in the kernel arguments
 struct ScoreParams {
-  int n_karg;                        // users of this launch with te_off_k (0 = read te_off)
-  long long te_off_k[kKargUsers + 1];  // te_off[user0 .. user0 + n_karg] (fused shape)
   int n_tr;
   int user0;
   int song_lo, song_hi, width;   // shard [lo, hi), width = hi - lo
@@ -967,10 +964,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
-  // T(u)'s offsets: from the kernel arguments when the launch's users fit them
-  // (scalar kernarg loads, one dependent global load fewer on stage 1's chain)
-  const bool karg = p.n_karg > 0 && bu < p.n_karg;
-  const long long t0 = karg ? p.te_off_k[bu] : p.te_off[u], t1 = karg ? p.te_off_k[bu + 1] : p.te_off[u + 1];
+  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
   // Prefetch this thread's epilogue scales (hidden behind stages 1-2): songs
   // tid + 256 j of the tile, j < kFusedPre (the whole tile up to 1024 songs).
   double sc[kFusedPre];
@@ -2221,8 +2215,6 @@ struct mr_ctx {
   int cap = 0, batch = 0;
   int chunk = 1, n_chunks = 1;  // separate shape: stage-1 chunks of train users
   size_t score_lds = 0, nbr_lds = 0, merge_lds = 0, wide_lds = 0;
-  std::vector<long long> h_te_off;  // host copy of te_off (kernel-argument offsets of the fused shape)
-  bool karg_te_off = true;          // MR_KARG_TE_OFF=0 disables (A/B experiments)
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
   NbrKernel nbr_kernel[2] = {nullptr, nullptr};
   ColKernel col_kernel[2] = {nullptr, nullptr};
@@ -2751,11 +2743,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
 
-  c->h_te_off.assign(d->te_off, d->te_off + n_te + 1);
-  {
-    const char* e = std::getenv("MR_KARG_TE_OFF");
-    c->karg_te_off = !(e && std::atoi(e) == 0);
-  }
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
   c->song_lo = lo; c->song_hi = hi; c->width = width;
   c->block_songs = bs; c->n_tiles = n_tiles;
@@ -2909,11 +2896,6 @@ int run_model(mr_ctx* c, int model) {
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
       sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused / user shapes (else null)
-      sp.n_karg = 0;
-      if (c->fused && c->karg_te_off && ny <= kKargUsers && !remap) {
-        sp.n_karg = ny;
-        for (int i = 0; i <= ny; ++i) sp.te_off_k[i] = c->h_te_off[user0 + y0 + i];
-      }
 #ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
       sp.te_rng = nullptr;
 #endif
