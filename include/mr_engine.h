@@ -170,6 +170,14 @@ int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_
 int mr_run(mr_ctx* ctx, int model);
 int mr_sync(mr_ctx* ctx);
 
+/* HIP graph of n_steps back-to-back mr_run(model) of this context (stream
+ * capture on the context stream; instantiated once, replaced by the next
+ * capture, released by mr_load / mr_destroy). mr_graph_launch replays it,
+ * asynchronous on the context stream: one launch for the n steps instead of n
+ * host launches. Outputs as after mr_run. Not with time_kernels = 1. */
+int mr_graph_capture(mr_ctx* ctx, int model, int32_t n_steps);
+int mr_graph_launch(mr_ctx* ctx);
+
 /* Device pointers of the last mr_run's outputs (valid until the next
  * mr_run/mr_load/mr_destroy). Any pointer may be NULL. */
 int mr_device_outputs(const mr_ctx* ctx, void** dense, int32_t** topk_songs,

@@ -126,6 +126,8 @@ SIGNATURES = {
     "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),
+    "mr_graph_capture": (c_int, [c_void_p, c_int, c_int32]),
+    "mr_graph_launch": (c_int, [c_void_p]),
     "mr_device_outputs": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),
     "mr_score_dense": (c_int, [c_void_p, c_int, c_void_p]),
     "mr_topk": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

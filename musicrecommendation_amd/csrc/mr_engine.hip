@@ -2246,6 +2246,9 @@ struct mr_ctx {
   hipEvent_t win[2] = {nullptr, nullptr};
   bool win_open = false;
   void* dense_override = nullptr;  // mr_run_into: caller's device buffer for this run's dense model
+  hipGraph_t graph = nullptr;          // mr_graph_capture: n steps of mr_run
+  hipGraphExec_t graph_exec = nullptr;
+  int graph_steps = 0;
   DevBuf<unsigned> flag;           // mr_topk_dense_device: negative-score flag
   long long win_launches = 0;
 
@@ -2261,6 +2264,11 @@ struct mr_ctx {
     yt.release();
     dbg.release();
     flag.release();
+    if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    graph_exec = nullptr;
+    graph = nullptr;
+    graph_steps = 0;
     loaded = ran = false;
   }
 };
@@ -2972,6 +2980,43 @@ int mr_run(mr_ctx* c, int model) {
   if (rc) return rc;
   c->ran = true;
   c->last_model = model;
+  return MR_OK;
+}
+
+int mr_graph_capture(mr_ctx* c, int model, int32_t n_steps) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_graph_capture before mr_load");
+  if (model != MR_UBM && model != MR_IBM) return fail(MR_E_INVALID, "unknown model %d", model);
+  if (n_steps < 1 || n_steps > 100000) return fail(MR_E_INVALID, "n_steps %d outside [1,100000]", n_steps);
+  if (c->opt.time_kernels) return fail(MR_E_STATE, "graph capture of a context with time_kernels=1");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  if (c->graph_exec) { MR_HIP(hipGraphExecDestroy(c->graph_exec)); c->graph_exec = nullptr; }
+  if (c->graph) { MR_HIP(hipGraphDestroy(c->graph)); c->graph = nullptr; }
+  c->graph_steps = 0;
+  MR_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  int rc = MR_OK;
+  const long long counted = c->win_launches;  // captured launches are not runs
+  for (int i = 0; i < n_steps && rc == MR_OK; ++i) rc = run_model(c, model);
+  c->win_launches = counted;
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(c->stream, &g);
+  if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return fail(MR_E_HIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  c->graph = g;
+  MR_HIP(hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0));
+  c->graph_steps = n_steps;
+  c->last_model = model;
+  return MR_OK;
+}
+
+int mr_graph_launch(mr_ctx* c) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->graph_exec) return fail(MR_E_STATE, "no captured graph (mr_graph_capture)");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MR_HIP(hipGraphLaunch(c->graph_exec, c->stream));
+  if (c->win_open) c->win_launches += c->graph_steps;
+  c->ran = true;
   return MR_OK;
 }
 

@@ -99,6 +99,14 @@ class Engine:
     def sync(self) -> None:
         _lib.check(self._L.mr_sync(self._h), "mr_sync")
 
+    def graph_capture(self, model: Union[str, int], n_steps: int) -> None:
+        """Capture n_steps back-to-back runs of `model` into a HIP graph."""
+        _lib.check(self._L.mr_graph_capture(self._h, model_id(model), int(n_steps)), "mr_graph_capture")
+
+    def graph_launch(self) -> None:
+        """Replay the captured graph (asynchronous on the engine stream)."""
+        _lib.check(self._L.mr_graph_launch(self._h), "mr_graph_launch")
+
     @property
     def stream(self) -> int:
         return self._L.mr_stream(self._h) or 0
