@@ -1507,18 +1507,49 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     load_offs(v0, a0, b0);
     load_list(tid + R * NT, v1, q1);
     for (int k0 = tid; k0 < cnt; k0 += R * NT) {
+#ifndef MR_WIDE_U16
+      // a segment's first kSeg entries as 8-B words (4 tile-local ids each)
+      // from the aligned word holding entry a0: kW loads instead of kSeg
+      // 2-B loads (C4 21.9 vs 22.9 ms per 704-user batch, C3 1.093 vs 1.141 ms
+      // per step; MR_WIDE_U16 builds the 2-B form, profiles/r02/c4/vec_seg_ab.txt)
+      constexpr int kW = (kSeg + 3) / 4 + 1;
+      const uint2* tw = reinterpret_cast<const uint2*>(p.tsongs);
+      uint2 sw[R][kW];
+      int so[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int wb = a0[r] >> 2;
+        const int we = b0[r] > a0[r] ? (b0[r] + 3) >> 2 : wb;
+        so[r] = a0[r] & 3;
+#pragma unroll
+        for (int j = 0; j < kW; ++j) sw[r][j] = wb + j < we ? tw[wb + j] : make_uint2(0u, 0u);
+      }
+#else
       int sg[R][kSeg];
 #pragma unroll
       for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < kSeg; ++j) sg[r][j] = a0[r] + j < b0[r] ? (int)p.tsongs[a0[r] + j] : -1;
+#endif
       load_offs(v1, a1, b1);                 // iteration i+1
       load_list(k0 + 2 * R * NT, v2, q2);    // iteration i+2
 #pragma unroll
       for (int r = 0; r < R; ++r) {
+#ifndef MR_WIDE_U16
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) {
+          if (a0[r] + j < b0[r]) {
+            const int e = (j & 3) + so[r];  // 0..6: word j/4 or the next one
+            const uint2 wv = e >= 4 ? sw[r][(j >> 2) + 1] : sw[r][j >> 2];
+            const unsigned x = ((e & 3) < 2 ? wv.x : wv.y) >> ((e & 1) * 16);
+            atomicAdd(&acc[x & 0xffffu], q0[r]);
+          }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < kSeg; ++j)
           if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q0[r]);
+#endif
         for (int x0 = a0[r] + kSeg; x0 < b0[r]; x0 += kSeg) {
           int st[kSeg];
 #pragma unroll
@@ -2628,7 +2659,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       if (s >= lo && s < hi) toff[(size_t)((s - lo) / bs) * n_tr + v + 1]++;
     }
   for (size_t i = 0; i < n_tv; ++i) toff[i + 1] += toff[i];
-  std::vector<uint16_t> tsongs(std::max<int64_t>(1, toff[n_tv]));
+  // padded to whole 8-B words (+1): the wide kernel loads a segment's ids as
+  // aligned 4-id words
+  std::vector<uint16_t> tsongs((std::max<int64_t>(1, toff[n_tv]) + 3) / 4 * 4 + 4);
   {
     std::vector<int32_t> fill(toff.begin(), toff.end() - 1);
     for (int v = 0; v < (pull ? 0 : n_tr); ++v)
