@@ -242,6 +242,11 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)
         step_bytes = 2 * model_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
         step_s = elapsed / args.steps
+        traffic = None
+        pmc_file = os.path.join(ROOT, "profiles", "pmc_c5.json")
+        if world == 1 and os.path.exists(pmc_file):  # per-step PMC sum (scripts/pmc_traffic.py step mode)
+            with open(pmc_file) as f:
+                traffic = json.load(f).get("traffic_bytes_per_launch")
         line = {
             "metric": "scored (test-user,song) pairs/sec, ensemble ubm+ibm+lcm+am+scm + threshold mAP",
             "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -254,7 +259,10 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
                        "parallelism": f"songs{gs}xusers{gu}"},
             "roofline": {"bound": "hbm", "kernel": "whole step (2 scoring passes + 3 combinations + 5 evaluations)",
                          "achieved": step_bytes / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": "profiles/pmc_c5.json (rocprofv3 --pmc passes over one step, every "
+                                           "engine kernel summed)" if traffic else None,
+                         "traffic_GBps": traffic / step_s / 1e9 if traffic else None,
                          "algorithmic_bytes_per_step": step_bytes},
             "threshold_mAP": maps,
             "mAP@10_lcm": evaluation.map_at_k(songs, full, 10) if world == 1 else None,
@@ -530,6 +538,8 @@ def main() -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                # measured fabric bytes over the same device time (traffic per launch ÷ avg_launch_us)
+                "traffic_GBps": traffic / (avg_us * 1e-6) / 1e9 if traffic else None,
                 "algorithmic_bytes_per_launch": ab_dom,
                 "avg_launch_us": avg_us,
                 "launches_per_step": launches_per_step,
