@@ -173,15 +173,32 @@ __device__ __forceinline__ void stamp_at(long long* sb, int i) {
 #define MR_STAMP(i) do {} while (0)
 #endif
 
+// Inclusive wave prefix sum. DPP (no LDS round trip): row_shr 1/2/4/8 scan
+// each row of 16 lanes (a source outside the row reads the 0 of `old`),
+// row_bcast 15 / 31 add the rows below. MR_NO_DPP: the ds_bpermute chain.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+#ifndef MR_NO_DPP
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+#else
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+#endif
+  return x;
+}
+
 // Block-wide exclusive scan of one int per thread (256 threads). `sbuf` holds kWaves ints.
 __device__ __forceinline__ int block_excl_scan(int x, int* total, int* sbuf) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int incl = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
+  const int incl = wave_incl_scan(x);
   if (lane == 63) sbuf[w] = incl;
   __syncthreads();
   int off = 0, tot = 0;
@@ -270,6 +287,29 @@ __device__ __forceinline__ void take_if_before(long long& ka, int& sa, long long
   const bool t = cand_before(kb, sb, ka, sa);
   ka = t ? kb : ka;
   sa = t ? sb : sa;
+}
+
+// (k, s) <- the better of itself and lane CTRL's (a DPP pattern whose sources
+// all lie in the row: quad_perm, row_mirror, row_half_mirror).
+template <int CTRL>
+__device__ __forceinline__ void dpp_take(long long& k, int& s) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(unsigned long long)k, CTRL, 0xf, 0xf,
+                                                            false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(k >> 32), CTRL, 0xf, 0xf, false);
+  const int os = __builtin_amdgcn_update_dpp(0, s, CTRL, 0xf, 0xf, false);
+  take_if_before(k, s, (long long)(((unsigned long long)(unsigned)hi << 32) | lo), os);
+}
+
+// Best of each aligned group of GS lanes (GS <= 16), in every lane of the
+// group: quad xor 1, quad xor 2, then the half-row and row mirrors pair the
+// quads and the half-rows. DPP: no LDS round trip per step.
+template <int GS>
+__device__ __forceinline__ void group_best(long long& k, int& s) {
+  static_assert(GS == 1 || GS == 2 || GS == 4 || GS == 8 || GS == 16, "group size");
+  if constexpr (GS >= 2) dpp_take<0xB1>(k, s);   // quad_perm [1,0,3,2]
+  if constexpr (GS >= 4) dpp_take<0x4E>(k, s);   // quad_perm [2,3,0,1]
+  if constexpr (GS >= 8) dpp_take<0x141>(k, s);  // row_half_mirror
+  if constexpr (GS >= 16) dpp_take<0x140>(k, s); // row_mirror
 }
 
 // Sort M register candidates of a lane descending (odd-even transposition).
@@ -557,11 +597,18 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   int* crank = grank + NG;                             // [256]
   const int tid = threadIdx.x, lane = tid & 63;
   if (k > NG || k <= 0 || cap > 256) return false;
+#ifndef MR_NO_DPP
+  if constexpr (GS <= 16) {
+    group_best<GS>(mk, ms);
+  } else
+#endif
+  {
 #pragma unroll
-  for (int d = 1; d < GS; d <<= 1) {
-    const long long ok = __shfl_xor(mk, d, 64);
-    const int os = __shfl_xor(ms, d, 64);
-    take_if_before(mk, ms, ok, os);
+    for (int d = 1; d < GS; d <<= 1) {
+      const long long ok = __shfl_xor(mk, d, 64);
+      const int os = __shfl_xor(ms, d, 64);
+      take_if_before(mk, ms, ok, os);
+    }
   }
   if ((lane & (GS - 1)) == 0) { gk[tid / GS] = mk; gs[tid / GS] = ms; }
   if (tid < NG) grank[tid] = 0;
@@ -1113,12 +1160,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int len = b0[r] - a0[r];
-        int incl = len;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const int y = __shfl_up(incl, d, 64);
-          if (lane >= d) incl += y;
-        }
+        const int incl = wave_incl_scan(len);
         const int it = r * 64 + lane;
         st_a[it] = a0[r];
         st_pre[it] = run + incl - len;
@@ -1355,12 +1397,7 @@ template <int NT>
 __device__ __forceinline__ int block_excl_scan_nt(int x, int* total, int* sbuf) {
   constexpr int NW = NT / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int incl = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
+  const int incl = wave_incl_scan(x);
   if (lane == 63) sbuf[w] = incl;
   __syncthreads();
   int off = 0, tot = 0;
