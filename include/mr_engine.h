@@ -121,7 +121,7 @@ typedef struct mr_options {
                           n_train_users >= 1e5, else fused; topk > 16: fused when
                           n_train_users <= 4096, else separate. Pull and user on request. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
-                          to 16384, else 8192); smaller values exercise the chunked path */
+                          to 16384, else 4096); smaller values exercise the chunked path */
   int32_t train_order; /* 0 (default) = train users renumbered internally by distinct-song count
                           (descending) for load balance; 1 = as given. Results are identical. */
   int32_t topk_lists;  /* 1 = tile top-k of the wide / user shapes by per-thread running lists only

@@ -53,8 +53,10 @@ constexpr int kMaxBlockSongs = 16384;     // 128 KiB of int64 accumulators (LDS 
 constexpr int kLdsBytes = 160 * 1024;     // LDS per workgroup (CU) on gfx950
 constexpr int kMaxWideBlockSongs = 65536; // wide shape: uint16 tile-local ids, LDS-bound in practice
 constexpr int kMaxLdsTrainUsers = 16384;  // stage-1 dense neighbour array in LDS (int64), one chunk
-constexpr int kStage1Chunk = 8192;        // larger train sets: stage 1 in LDS chunks of train users
-constexpr int kMaxChunks = 1024;          // => n_train_users <= 8.4M
+constexpr int kStage1Chunk = 4096;        // larger train sets: stage 1 in LDS chunks of train users (C4
+                                          // batch 21.3 vs 21.9 ms at 8192, 23.8 at 16384, 22.5 at 2048;
+                                          // profiles/r02/c4/stage1_chunk_sweep.txt)
+constexpr int kMaxChunks = 2048;          // => n_train_users <= 8.4M
 constexpr int kMaxFusedTrainUsers = 4096; // fused path: Y (32 KiB) + tile live together
 constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doubles >= 0
 constexpr int kMaxTopkTile = 1024;        // songs per tile for the register top-k (4 per lane)

@@ -127,7 +127,7 @@ def test_wide_shape_small_inputs(model, chunk, k):
 
 @pytest.mark.parametrize("model", MODELS)
 def test_large_train_set_exact(model):
-    """n_train > 16384: chunked stage 1 (8192 train users per LDS chunk),
+    """n_train > 16384: chunked stage 1 (4096 train users per LDS chunk),
     16384-song tiles, XCD-grouped tiles; every user exact vs the oracle."""
     ds = synth.generate_bulk(40_000, 21, 4).dataset()
     with Engine(ds, out_dtype="f64", topk=10) as e:
