@@ -345,6 +345,8 @@ def main() -> None:
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="users shard, small configs: replay the K timed steps as one captured HIP graph "
                          "(--no-graph: K stream launches)")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps per captured graph (must divide --steps; 0 = all K in one graph)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -432,8 +434,10 @@ def main() -> None:
     if args.shard == "users" and not bulk:
         step_i[0] = 0
     use_graph = args.graph and args.shard == "users" and not bulk and args.inflight == 1
-    if use_graph:  # the K timed steps as one HIP graph (captured untimed, replayed once)
-        eng.graph_capture(args.model, args.steps)
+    g_steps = args.graph_steps if 0 < args.graph_steps <= args.steps and args.steps % args.graph_steps == 0 \
+        else args.steps
+    if use_graph:  # the K timed steps as K / G replays of a G-step HIP graph (captured untimed)
+        eng.graph_capture(args.model, g_steps)
         eng.graph_launch()  # first replay uploads the graph: untimed
         drain()
     if world > 1:
@@ -442,10 +446,12 @@ def main() -> None:
     t0 = time.perf_counter()
     eng.timing_begin()  # HIP events on the engine's own stream, around the timed steps
     if use_graph:
-        eng.graph_launch()
+        for _ in range(args.steps // g_steps):
+            eng.graph_launch()
     else:
         for _ in range(args.steps):
             step()
+    t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
     n_launch, win_ms = eng.timing_end()
     drain()
     torch.cuda.synchronize()
@@ -523,7 +529,9 @@ def main() -> None:
                 "parallelism": (f"users{world}" if args.shard == "users" and not bulk
                                 else f"songs{scorer.gs}xusers{scorer.gu}"),
                 "inflight": args.inflight,
-                "launch": "hip graph of the K steps" if use_graph else "stream launches",
+                "launch": (f"hip graph of {g_steps} steps x {args.steps // g_steps}" if use_graph
+                           else "stream launches"),
+                "host_submit_ms": t_submit * 1e3,
             },
             "roofline": {
                 "bound": "hbm",
