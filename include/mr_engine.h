@@ -269,6 +269,12 @@ int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, 
  * #test users whose labels hold s. */
 int mr_eval_map(int32_t n_classes, const int32_t* pred_counts, const int32_t* tp_counts, const int32_t* pos,
                 int32_t n_label_songs, double* map_out);
+/* The two above in one call for a context that holds every test user: counts
+ * and the per-class AP on the device (the same double operations), only the
+ * AP per class crosses PCIe, summed on the host in song-id order — bit-equal
+ * to mr_eval_counts_device + mr_eval_map. pos: host [>= song_hi], global. */
+int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
  * (0 = separate stage-1 kernel — neighbour lists or pull columns —, 1 = the

@@ -244,11 +244,93 @@ __global__ __launch_bounds__(kThreads) void k_eval_tp(EvalParams p) {
   for (int t = 0; t < c; ++t) atomicAdd(&p.tp[(size_t)g * kThresholds + t], 1);
 }
 
+// AP of every song class of the shard (MR:588-618), the host fold's exact
+// double operations (mr_eval_map) per class; classes nobody holds get 0.
+__global__ __launch_bounds__(kThreads) void k_eval_ap(int width, int song_lo, const int* pred, const int* tp,
+                                                      const int* pos, double* ap) {
+  const int g = blockIdx.x * kThreads + threadIdx.x;
+  if (g >= width) return;
+  const int np = pos[g];
+  if (np <= 0) { ap[g] = 0.0; return; }
+  double P[kThresholds], R[kThresholds];
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t) {
+    const size_t i = (size_t)g * kThresholds + t;
+    P[t] = pred[i] > 0 ? (double)tp[i] / (double)pred[i] : 0.0;
+    R[t] = (double)tp[i] / (double)np;
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int t = 0; t < kThresholds; ++t) {
+    const double term = t == 9 ? 0.0 : t == 8 ? (R[8] - 0.0) * P[8] : (R[t] - R[t + 1]) * P[t];
+    a = a + term;
+  }
+  ap[g] = a;
+  (void)song_lo;
+}
+
 template <typename T>
-struct Tmp {  // scratch device buffer of one call
+struct Tmp {  // scratch device buffer of one call, stream-ordered (pool allocator: no device sync)
   T* p = nullptr;
-  ~Tmp() { if (p) (void)hipFree(p); }
+  hipStream_t st = nullptr;
+  ~Tmp() { if (p) (void)hipFreeAsync(p, st); }
 };
+
+// pred / tp counts of the shard into the device buffers d_pred / d_tp
+// ([width][10], stream-ordered on the context stream; the caller frees them).
+int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                const int32_t* lab_songs, mr_view& v, Tmp<int>& d_pred, Tmp<int>& d_tp) {
+  if (!ctx || !dense || !lab_off) return fail(MR_E_INVALID, "null argument");
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  MR_HIP(hipSetDevice(v.device));
+  const int width = v.song_hi - v.song_lo, n_te = v.n_test_users;
+  const long long n_lab = lab_off[n_te];
+  if (n_lab > 0 && !lab_songs) return fail(MR_E_INVALID, "null label songs");
+  std::vector<int32_t> lu((size_t)std::max<long long>(1, n_lab)), ls((size_t)std::max<long long>(1, n_lab));
+  for (int u = 0; u < n_te; ++u)
+    for (int64_t j = lab_off[u]; j < lab_off[u + 1]; ++j) {
+      if (j < 0 || j >= n_lab || lab_off[u + 1] < lab_off[u]) return fail(MR_E_INVALID, "bad label CSR");
+      lu[j] = u;
+      ls[j] = lab_songs[j];
+    }
+  hipStream_t st = (hipStream_t)v.stream;
+  Tmp<int> d_lu, d_ls;
+  d_pred.st = d_tp.st = d_lu.st = d_ls.st = st;
+  const size_t nc = (size_t)width * kThresholds;
+  MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_pred.p), std::max<size_t>(1, nc) * 4, st));
+  MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_tp.p), std::max<size_t>(1, nc) * 4, st));
+  MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_lu.p), lu.size() * 4, st));
+  MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ls.p), ls.size() * 4, st));
+  MR_HIP(hipMemsetAsync(d_pred.p, 0, nc * 4, st));
+  MR_HIP(hipMemsetAsync(d_tp.p, 0, nc * 4, st));
+  MR_HIP(hipMemcpyAsync(d_lu.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, st));
+  MR_HIP(hipMemcpyAsync(d_ls.p, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, st));
+  // enough (song block x user block) workgroups to fill the chip
+  const int sx = (width + kThreads - 1) / kThreads;
+  const int uy = std::max(1, std::min((n_te + 31) / 32, (8192 + sx - 1) / sx));
+  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
+                n_lab};
+  const bool f64 = v.out_dtype == MR_OUT_F64;
+  for (int t = 0; t < kThresholds; ++t) {
+    const double thr = kThrHost[t];
+    ep.xt_f[t] = level_floor<float, uint32_t>(mn, mx, thr);
+    ep.xt_d[t] = level_floor<double, uint64_t>(mn, mx, thr);
+  }
+  if (width > 0) {
+    if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+    else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+    MR_HIP(hipGetLastError());
+  }
+  if (n_lab > 0) {
+    const int lb = (int)((n_lab + kThreads - 1) / kThreads);
+    if (f64) hipLaunchKernelGGL(k_eval_tp<double>, dim3(lb), dim3(kThreads), 0, st, ep);
+    else hipLaunchKernelGGL(k_eval_tp<float>, dim3(lb), dim3(kThreads), 0, st, ep);
+    MR_HIP(hipGetLastError());
+  }
+  // the label staging is freed in stream order after these kernels (Tmp)
+  return MR_OK;
+}
 
 }  // namespace
 
@@ -322,57 +404,46 @@ int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx
 
 int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
                           const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts) {
-  if (!ctx || !dense || !lab_off || !pred_counts || !tp_counts) return fail(MR_E_INVALID, "null argument");
+  if (!pred_counts || !tp_counts) return fail(MR_E_INVALID, "null argument");
   mr_view v;
-  int rc = mr_view_get(ctx, &v);
+  Tmp<int> d_pred, d_tp;
+  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, v, d_pred, d_tp);
   if (rc) return rc;
-  MR_HIP(hipSetDevice(v.device));
-  const int width = v.song_hi - v.song_lo, n_te = v.n_test_users;
-  const long long n_lab = lab_off[n_te];
-  if (n_lab > 0 && !lab_songs) return fail(MR_E_INVALID, "null label songs");
-  std::vector<int32_t> lu((size_t)std::max<long long>(1, n_lab)), ls((size_t)std::max<long long>(1, n_lab));
-  for (int u = 0; u < n_te; ++u)
-    for (int64_t j = lab_off[u]; j < lab_off[u + 1]; ++j) {
-      if (j < 0 || j >= n_lab || lab_off[u + 1] < lab_off[u]) return fail(MR_E_INVALID, "bad label CSR");
-      lu[j] = u;
-      ls[j] = lab_songs[j];
-    }
-  Tmp<int> d_pred, d_tp, d_lu, d_ls;
-  const size_t nc = (size_t)width * kThresholds;
-  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_pred.p), std::max<size_t>(1, nc) * 4));
-  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_tp.p), std::max<size_t>(1, nc) * 4));
-  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_lu.p), lu.size() * 4));
-  MR_HIP(hipMalloc(reinterpret_cast<void**>(&d_ls.p), ls.size() * 4));
   hipStream_t st = (hipStream_t)v.stream;
-  MR_HIP(hipMemsetAsync(d_pred.p, 0, nc * 4, st));
-  MR_HIP(hipMemsetAsync(d_tp.p, 0, nc * 4, st));
-  MR_HIP(hipMemcpyAsync(d_lu.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, st));
-  MR_HIP(hipMemcpyAsync(d_ls.p, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, st));
-  // enough (song block x user block) workgroups to fill the chip
-  const int sx = (width + kThreads - 1) / kThreads;
-  const int uy = std::max(1, std::min((n_te + 31) / 32, (8192 + sx - 1) / sx));
-  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
-                n_lab};
-  const bool f64 = v.out_dtype == MR_OUT_F64;
-  for (int t = 0; t < kThresholds; ++t) {
-    const double thr = kThrHost[t];
-    ep.xt_f[t] = level_floor<float, uint32_t>(mn, mx, thr);
-    ep.xt_d[t] = level_floor<double, uint64_t>(mn, mx, thr);
-  }
-  if (width > 0) {
-    if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
-    else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
-    MR_HIP(hipGetLastError());
-  }
-  if (n_lab > 0) {
-    const int lb = (int)((n_lab + kThreads - 1) / kThreads);
-    if (f64) hipLaunchKernelGGL(k_eval_tp<double>, dim3(lb), dim3(kThreads), 0, st, ep);
-    else hipLaunchKernelGGL(k_eval_tp<float>, dim3(lb), dim3(kThreads), 0, st, ep);
-    MR_HIP(hipGetLastError());
-  }
+  const size_t nc = (size_t)(v.song_hi - v.song_lo) * kThresholds;
   MR_HIP(hipMemcpyAsync(pred_counts, d_pred.p, nc * 4, hipMemcpyDeviceToHost, st));
   MR_HIP(hipMemcpyAsync(tp_counts, d_tp.p, nc * 4, hipMemcpyDeviceToHost, st));
   MR_HIP(hipStreamSynchronize(st));
+  return MR_OK;
+}
+
+int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out) {
+  if (!pos || !map_out) return fail(MR_E_INVALID, "null argument");
+  mr_view v;
+  Tmp<int> d_pred, d_tp;
+  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, v, d_pred, d_tp);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)v.stream;
+  const int width = v.song_hi - v.song_lo;
+  Tmp<int> d_pos;
+  Tmp<double> d_ap;
+  d_pos.st = d_ap.st = st;
+  std::vector<double> ap((size_t)std::max(1, width));
+  if (width > 0) {
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_pos.p), (size_t)width * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)width * 8, st));
+    MR_HIP(hipMemcpyAsync(d_pos.p, pos + v.song_lo, (size_t)width * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_eval_ap, dim3((width + kThreads - 1) / kThreads), dim3(kThreads), 0, st, width, v.song_lo,
+                       d_pred.p, d_tp.p, d_pos.p, d_ap.p);
+    MR_HIP(hipGetLastError());
+    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)width * 8, hipMemcpyDeviceToHost, st));
+    MR_HIP(hipStreamSynchronize(st));
+  }
+  double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
+  for (int g = 0; g < width; ++g)
+    if (pos[v.song_lo + g] > 0) total += ap[g];
+  *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
   return MR_OK;
 }
 

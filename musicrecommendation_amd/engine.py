@@ -198,6 +198,22 @@ class Engine:
             tp.ctypes.data_as(ctypes.c_void_p)), "mr_eval_counts_device")
         return pred, tp
 
+    def eval_map(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray, lab_songs: np.ndarray,
+                 pos: np.ndarray, n_label_songs: int) -> float:
+        """Threshold mAP with counts and per-class AP on the device
+        (mr_eval_map_device; the context must hold every test user)."""
+        lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
+        lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
+        pos = np.ascontiguousarray(pos, dtype=np.int32)
+        if pos.shape[0] < self.song_hi:
+            raise ValueError("pos must cover the shard's songs")
+        out = ctypes.c_double()
+        _lib.check(self._L.mr_eval_map_device(
+            self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
+            lab_songs.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p), int(n_label_songs),
+            ctypes.byref(out)), "mr_eval_map_device")
+        return out.value
+
     def timing_begin(self) -> None:
         """Open a timing window (one event on the engine stream)."""
         _lib.check(self._L.mr_timing_begin(self._h), "mr_timing_begin")

@@ -191,3 +191,23 @@ def test_level_thresholds_exact_at_boundaries(dtype):
                            axis=1)
         assert np.array_equal(pred, exp.astype(np.int32))
         assert ens.threshold_map(t) == evaluation.threshold_map(xd, ds)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_device_map_fold_equals_host_fold(dtype):
+    """mr_eval_map_device (counts + AP per class on the device, ordered host sum)
+    == mr_eval_counts_device + mr_eval_map, bit for bit, and both == numpy."""
+    from musicrecommendation_amd.ensemble import eval_map
+
+    for name, ds in datasets():
+        with Engine(ds, out_dtype=dtype, topk=4) as e:
+            ens = DeviceEnsemble(e)
+            for t in (ens.model("ubm"), ens.model("ibm")):
+                mn, mx = e.eval_minmax(t.data_ptr())
+                pred, tp = e.eval_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs)
+                host = eval_map(pred, tp, ens.pos, ds.n_label_songs)
+                dev = e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, ens.pos, ds.n_label_songs)
+                assert dev == host, name
+                assert dev == evaluation.threshold_map(t.cpu().numpy().astype(np.float64), ds), name
+            with pytest.raises(ValueError):
+                e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, ens.pos[:1], ds.n_label_songs)
