@@ -1,0 +1,10 @@
+#!/bin/bash
+# full GPU suite + smoke + default C2 bench on the current tree (toff pair as one 8-B load, packed neighbour
+# records), then C4/C3 A/B: default vs nopack (MR_NBR_NOPACK) vs split (neither change)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+bash scripts/session_last.sh || exit $?
+OUT=gpurun_out/r2ba; mkdir -p $OUT
+export TMPDIR=/tmp
+for rep in 1 2; do for v in "" nopack split; do MR_ENGINE_LIB=$v timeout -k 10 300 python scripts/c4_probe.py 704 > $OUT/c4_$v.json 2>&1; rc=$?; echo "c4 [$v] $(tail -1 $OUT/c4_$v.json | grep -o '"device_ms": [0-9.]*')"; [ $rc -eq 0 ] || exit $rc; done; done
+for rep in 1 2; do for v in "" nopack split; do MR_ENGINE_LIB=$v timeout -k 10 300 python bench.py --config c3 --steps 20 --warmup 3 --no-cpu-baseline --no-e2e > $OUT/c3_$v.json 2>&1; rc=$?; echo "c3 [$v] $(grep -o '"ms_per_step": [0-9.]*' $OUT/c3_$v.json)"; [ $rc -eq 0 ] || exit $rc; done; done
