@@ -6,6 +6,7 @@ neighbour batch of the wide shape) — so a rocprofv3 --pmc pass sees one
 k_neighbours + one k_score_wide + one k_topk_merge dispatch per run.
   python scripts/c4_probe.py [N_USERS] [model]      timing (+ JSON on stdout)
   MR_PROBE_CHUNK=C ...                              stage-1 chunk of C train users
+  MR_PROBE_BS=B ...                                 song tiles of B songs
   MR_PROBE_BYTES=1 ...                              + the byte model per dispatch:
       algorithmic and the wide kernel's per-(neighbour, tile)
       index re-walk (nbr_v 4 B + nbr_q 8 B + toff pair 8 B, x n_tiles)."""
@@ -69,7 +70,8 @@ def main():
     full = c4_dataset()
     t1 = time.time()
     ds = full.subset_test_users(0, n)
-    with Engine(ds, topk=10, dense=False, stage1_chunk=int(os.environ.get("MR_PROBE_CHUNK", "0"))) as e:
+    with Engine(ds, topk=10, dense=False, stage1_chunk=int(os.environ.get("MR_PROBE_CHUNK", "0")),
+                block_songs=int(os.environ.get("MR_PROBE_BS", "0"))) as e:
         t2 = time.time()
         e.run(model)
         e.sync()
