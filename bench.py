@@ -342,6 +342,7 @@ def main() -> None:
                          "steps are issued round-robin, so up to this many overlap on the device")
     ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "pull", "wide", "user"],
                     help="launch shape (default: the engine's choice)")
+    ap.add_argument("--block-songs", type=int, default=0, help="songs per tile (default: the engine's choice)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="users shard, small configs: replay the K timed steps as one captured HIP graph "
                          "(--no-graph: K stream launches)")
@@ -388,7 +389,8 @@ def main() -> None:
         full = synth.config(args.config, n_test=n_te * nb).dataset()
         blocks = [full.subset_test_users(b * n_te, (b + 1) * n_te)
                   for b in range(rank * args.inflight, (rank + 1) * args.inflight)]
-        engines = [Engine(b, device=local, out_dtype="f32", topk=10, stage1=args.stage1) for b in blocks]
+        engines = [Engine(b, device=local, out_dtype="f32", topk=10, stage1=args.stage1, block_songs=args.block_songs)
+                   for b in blocks]
         ds = blocks[0]
         eng = engines[0]
         pairs_per_engine = [b.n_pairs() for b in blocks]
@@ -413,7 +415,7 @@ def main() -> None:
 
         full = synth.config(args.config, n_test=None if bulk else n_te * world).dataset()
         scorer = ShardScorer(full, rank, world, local, song_groups=song_groups_for(args, world), topk=10,
-                             out_dtype="f32", dense=dense_out, stage1=args.stage1)
+                             out_dtype="f32", dense=dense_out, stage1=args.stage1, block_songs=args.block_songs)
         eng = scorer.engine
         ds = scorer.ds
         engines = [eng]

@@ -122,7 +122,7 @@ class ShardScorer:
 
     def __init__(self, ds: Dataset, rank: int, world: int, device: int, *, song_groups: Optional[int] = None,
                  topk: int = 10, dense: bool = True, out_dtype: str = "f32", time_kernels: bool = False,
-                 stage1: str = "auto"):
+                 stage1: str = "auto", block_songs: int = 0):
         import torch
         from .engine import Engine
 
@@ -135,7 +135,8 @@ class ShardScorer:
         self.ds = ds if self.gu == 1 else ds.subset_test_users(self.user_lo, self.user_hi)
         self.group = block_group(rank, world, self.gs) if world > 1 else None
         self.engine = Engine(self.ds, device=device, song_lo=self.song_lo, song_hi=self.song_hi, topk=topk,
-                             dense=dense, out_dtype=out_dtype, time_kernels=time_kernels, stage1=stage1)
+                             dense=dense, out_dtype=out_dtype, time_kernels=time_kernels, stage1=stage1,
+                             block_songs=block_songs)
         self.device = torch.device("cuda", device)
         n_te = self.ds.n_test
         self.local_songs = torch.empty((n_te, topk), dtype=torch.int32, device=self.device)
