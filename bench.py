@@ -192,13 +192,13 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     are per pair, the mAP reductions (MIN/MAX, count SUM) go over RCCL."""
     from musicrecommendation_amd import evaluation
     from musicrecommendation_amd.ensemble import DeviceEnsemble
-    from musicrecommendation_amd.sharding import layout_2d, song_shards, user_blocks
+    from musicrecommendation_amd.sharding import layout_2d, shard_tile, song_shards, user_blocks
 
     n_tr, n_te, _seed = synth.BULK_CONFIGS["c5"]
     full = synth.config("c5").dataset()
     gs, gu = layout_2d(world, song_groups_for(args, world))
     a, b = user_blocks(full.n_test, gu)[rank // gs]
-    lo, hi = song_shards(full, gs)[rank % gs]
+    lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu))[rank % gs]
     ds = full if gu == 1 else full.subset_test_users(a, b)
     eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi)
     ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),

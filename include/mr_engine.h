@@ -158,6 +158,16 @@ int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int3
  * the train users (*n_chunks chunks of *chunk users). */
 int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_chunks);
 
+/* Host only, before any load: the song tile of the wide shape that a context
+ * with these options would use for n_train_users x n_test_users (the widest
+ * the LDS holds, or opt->block_songs when set; opt = NULL: the defaults), or
+ * *tile_songs = 0 when mr_load would pick another shape. The wide kernel's
+ * unit of work is one walk of a test user's neighbour list per tile, so song
+ * shards cut at multiples of it (mr_song_shards_tiled) carry no partial
+ * tile: the multi-GPU layouts' per-GPU work (distributed.scala:477-479). */
+int mr_shard_tile_songs(const mr_options* opt, int32_t n_train_users, int32_t n_test_users,
+                        int32_t* tile_songs);
+
 /*
  * Score every (test user, song) pair of the shard for `model`, leaving the
  * results in device buffers (asynchronous on the context stream):
@@ -342,6 +352,11 @@ typedef struct mr_group mr_group;
 /* Host helper (no GPU): the group's song-range shard boundaries, bounds[0..n_shards]
  * (bounds[0] = 0, bounds[n_shards] = n_songs), balancing sum(c_tr(s) + 1). */
 int mr_song_shards(const mr_dataset* d, int32_t n_shards, int32_t* bounds);
+/* The same balance, then every shard narrowed to at most
+ * ceil(ceil(n_songs / tile_songs) / n_shards) tiles of tile_songs (each
+ * boundary moved the least from the balanced one); tile_songs <= 0: as
+ * mr_song_shards. mr_group_load uses it with mr_shard_tile_songs. */
+int mr_song_shards_tiled(const mr_dataset* d, int32_t n_shards, int32_t tile_songs, int32_t* bounds);
 
 int mr_group_options_default(mr_group_options* gopt);
 /* opt: the contexts' options (song_lo/song_hi must be 0: the group sets them). */

@@ -124,6 +124,7 @@ SIGNATURES = {
     "mr_shard_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_launch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "mr_shard_tile_songs": (c_int, [POINTER(MrOptions), c_int32, c_int32, POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),
     "mr_graph_capture": (c_int, [c_void_p, c_int, c_int32]),
@@ -165,6 +166,7 @@ SIGNATURES = {
     "mr_model_read_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "mr_java_double_string": (c_int, [c_double, c_char_p, c_int32]),
     "mr_song_shards": (c_int, [POINTER(MrDataset), c_int32, c_void_p]),
+    "mr_song_shards_tiled": (c_int, [POINTER(MrDataset), c_int32, c_int32, c_void_p]),
     "mr_group_options_default": (c_int, [POINTER(MrGroupOptions)]),
     "mr_group_create": (c_int, [POINTER(MrOptions), POINTER(MrGroupOptions), POINTER(c_void_p)]),
     "mr_group_destroy": (c_int, [c_void_p]),

@@ -2441,6 +2441,36 @@ int pull_range(int width, int batch) {
   return (int)std::max<long long>(64, std::min<long long>(r, 8192));
 }
 
+// Launch-shape rule of mr_load (also answers mr_shard_tile_songs before any
+// load). auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt):
+// wide beats separate and pull above 4096 train users, and fused from ~1e5
+// (test user x train user) pairs; fused for small sets (C2).
+int pick_shape(const mr_options& o, int n_tr, int n_te, bool user_fits) {
+  const int k = o.topk;
+  if (o.stage1 == 1) return kShapeFused;
+  if (o.stage1 == 2) return kShapeSeparate;
+  if (o.stage1 == 3) return kShapePull;
+  if (o.stage1 == 4) return kShapeWide;
+  if (o.stage1 == 5) return kShapeUser;
+  if (n_tr > kMaxFusedTrainUsers && k <= kMaxTopkLarge) return kShapeWide;
+  if ((long long)n_te * n_tr >= kWideMinUserPairs && k <= kMaxTopkLarge) return kShapeWide;
+  if (user_fits && kUserAuto) return kShapeUser;
+  return n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
+}
+
+// Train users per stage-1 chunk (separate / wide shapes).
+int stage1_chunk_for(const mr_options& o, int n_tr) {
+  return o.stage1_chunk > 0 ? std::min(o.stage1_chunk, std::max(1, n_tr))
+         : n_tr <= kMaxLdsTrainUsers ? std::max(1, n_tr) : kStage1Chunk;
+}
+
+// The widest wide-shape tile (a multiple of 256 songs) whose LDS fits one CU.
+int wide_bmax(int k, int n_chunks) {
+  int bmax = 256;
+  while (bmax + 256 <= 65536 && wide_lds<kWideThreads>(bmax + 256, k, n_chunks).total <= kLdsBytes) bmax += 256;
+  return bmax;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2607,19 +2637,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const int k = c->opt.topk;
   const bool user_fits = k <= kMaxTopkLarge && n_tr <= kMaxFusedTrainUsers && width <= kMaxWideBlockSongs &&
                          user_lds<kWideThreads>((width + 255) / 256 * 256, n_tr, k).total <= kLdsBytes;
-  int shape;
-  if (c->opt.stage1 == 1) shape = kShapeFused;
-  else if (c->opt.stage1 == 2) shape = kShapeSeparate;
-  else if (c->opt.stage1 == 3) shape = kShapePull;
-  else if (c->opt.stage1 == 4) shape = kShapeWide;
-  else if (c->opt.stage1 == 5) shape = kShapeUser;
-  // auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt):
-  // wide beats separate and pull above 4096 train users, and fused from ~1e5
-  // (test user x train user) pairs; fused for small sets (C2)
-  else if (n_tr > kMaxFusedTrainUsers && k <= kMaxTopkLarge) shape = kShapeWide;
-  else if ((long long)n_te * n_tr >= kWideMinUserPairs && k <= kMaxTopkLarge) shape = kShapeWide;
-  else if (user_fits && kUserAuto) shape = kShapeUser;
-  else shape = n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
+  const int shape = pick_shape(c->opt, n_tr, n_te, user_fits);
   const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide,
              user = shape == kShapeUser;
   const int user_bs = (width + 255) / 256 * 256;
@@ -2638,8 +2656,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (pull && n_tr > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "pull shape needs n_train_users <= %d (got %d)", kMaxLdsTrainUsers, n_tr);
   // Stage 1 of the separate shape: one LDS chunk of train users per workgroup.
-  const int chunk = c->opt.stage1_chunk > 0 ? std::min(c->opt.stage1_chunk, std::max(1, n_tr))
-                    : n_tr <= kMaxLdsTrainUsers ? std::max(1, n_tr) : kStage1Chunk;
+  const int chunk = stage1_chunk_for(c->opt, n_tr);
   if ((n_tr + chunk - 1) / chunk > kMaxChunks)
     return fail(MR_E_INVALID, "stage1_chunk %d gives more than %d chunks", chunk, kMaxChunks);
   const int n_chunks = (std::max(1, n_tr) + chunk - 1) / chunk;
@@ -2659,8 +2676,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // the widest tile the LDS holds (every tile re-walks the user's whole
       // neighbour list), then balanced: n_tiles = ceil(width / max), bs =
       // ceil(width / n_tiles) rounded up to 256
-      int bmax = 256;
-      while (bmax + 256 <= 65536 && wide_lds<kWideThreads>(bmax + 256, k, n_chunks).total <= kLdsBytes) bmax += 256;
+      const int bmax = wide_bmax(k, n_chunks);
       const long long nt = ((long long)width + bmax - 1) / bmax;
       bs = c->opt.block_songs > 0 ? c->opt.block_songs
                                   : (int)std::min<long long>(bmax, (((long long)width + nt - 1) / nt + 255) / 256 * 256);
@@ -2857,6 +2873,20 @@ int mr_batch_info(const mr_ctx* c, int32_t* batch, int32_t* chunk, int32_t* n_ch
   if (batch) *batch = c->batch;
   if (chunk) *chunk = c->chunk;
   if (n_chunks) *n_chunks = c->n_chunks;
+  return MR_OK;
+}
+
+int mr_shard_tile_songs(const mr_options* opt, int32_t n_train_users, int32_t n_test_users, int32_t* tile_songs) {
+  if (!tile_songs) return fail(MR_E_INVALID, "null output pointer");
+  mr_options o;
+  if (opt) o = *opt; else mr_options_default(&o);
+  if (n_train_users < 0 || n_test_users <= 0)
+    return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d", n_train_users, n_test_users);
+  *tile_songs = 0;
+  if (pick_shape(o, n_train_users, n_test_users, false) != kShapeWide || o.topk > kMaxTopkLarge) return MR_OK;
+  const int chunk = stage1_chunk_for(o, n_train_users);
+  const int n_chunks = (std::max(1, n_train_users) + chunk - 1) / chunk;
+  *tile_songs = o.block_songs > 0 ? o.block_songs : wide_bmax(o.topk, n_chunks);
   return MR_OK;
 }
 

@@ -183,7 +183,13 @@ namespace {
 
 // Song-range shards with ~equal Σ_s (c_tr(s) + 1) (stage-2 entries + one output
 // per song) — the same rule as sharding.song_shards.
-std::vector<int> song_bounds(const mr_dataset* d, int n) {
+// Shard boundaries balancing sum(c_tr(s) + 1) (sharding.song_shards); with
+// tile > 0 each boundary then moves the least so that no shard is wider than
+// M tiles, M = ceil(ceil(n_songs / tile) / n): the wide kernel's work is one
+// neighbour-list walk per (test user, tile), so a shard a few songs past a
+// whole number of tiles pays a whole extra tile (C4 4 x 2: 6 tiles on one
+// shard, 51.0 vs 47.5 ms per rank, profiles/r02/layouts_c4.txt).
+std::vector<int> song_bounds(const mr_dataset* d, int n, int tile = 0) {
   std::vector<long long> cost(d->n_songs, 1);
   for (int64_t i = 0; i < d->tr_off[d->n_train_users]; ++i) cost[d->tr_songs[i]]++;
   for (int s = 1; s < d->n_songs; ++s) cost[s] += cost[s - 1];
@@ -197,6 +203,16 @@ std::vector<int> song_bounds(const mr_dataset* d, int n) {
     b.push_back(std::min(std::max(i + 1, b.back() + 1), d->n_songs - (n - g)));
   }
   b.push_back(d->n_songs);
+  if (tile > 0) {
+    const long long n_s = d->n_songs, tiles = (n_s + tile - 1) / tile;
+    const long long cap = (tiles + n - 1) / n * tile;  // songs per shard at most
+    for (int g = 1; g < n; ++g) {
+      long long x = std::max<long long>(b[g], n_s - (long long)(n - g) * cap);
+      x = std::min<long long>(x, b[g - 1] + cap);
+      x = std::max<long long>(x, b[g - 1] + 1);
+      b[g] = (int)std::min<long long>(x, n_s - (n - g));
+    }
+  }
   return b;
 }
 
@@ -312,6 +328,14 @@ int mr_song_shards(const mr_dataset* d, int32_t n_shards, int32_t* bounds) {
   return MR_OK;
 }
 
+int mr_song_shards_tiled(const mr_dataset* d, int32_t n_shards, int32_t tile_songs, int32_t* bounds) {
+  const int rc = mr_song_shards(d, n_shards, bounds);
+  if (rc || tile_songs <= 0) return rc;
+  const std::vector<int> b = song_bounds(d, n_shards, tile_songs);
+  std::copy(b.begin(), b.end(), bounds);
+  return MR_OK;
+}
+
 int mr_group_options_default(mr_group_options* g) {
   if (!g) return gfail(MR_E_INVALID, "null group options");
   std::memset(g, 0, sizeof *g);
@@ -416,7 +440,9 @@ int mr_group_load(mr_group* g, const mr_dataset* d) {
   int rc = sync_all(g);
   if (rc) return rc;
   g->loaded = g->ran = false;
-  const std::vector<int> sb = song_bounds(d, g->gs());
+  int tile = 0;  // the wide shape's tile when the contexts will use it (mr_shard_tile_songs)
+  if (int rc = mr_shard_tile_songs(&g->opt, d->n_train_users, d->n_test_users / g->gu(), &tile)) return rc;
+  const std::vector<int> sb = song_bounds(d, g->gs(), tile);
   // Per user block: a view of the dataset over its test users (te_off rebased).
   std::vector<std::vector<int64_t>> te_off(g->gu());
   std::vector<mr_dataset> views(g->gu(), *d);

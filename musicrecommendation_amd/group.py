@@ -22,12 +22,17 @@ from .engine import model_id
 TRANSPORTS = {"auto": _lib.MR_TRANSPORT_AUTO, "copy": _lib.MR_TRANSPORT_COPY, "rccl": _lib.MR_TRANSPORT_RCCL}
 
 
-def song_shards_native(ds: Dataset, n_shards: int) -> List[Tuple[int, int]]:
-    """The group's shard boundaries (mr_song_shards; host only)."""
+def song_shards_native(ds: Dataset, n_shards: int, tile: int = 0) -> List[Tuple[int, int]]:
+    """The group's shard boundaries (mr_song_shards / mr_song_shards_tiled; host only)."""
     L = _lib.lib()
     cd = ds.c_struct()
     b = np.empty(n_shards + 1, dtype=np.int32)
-    _lib.check(L.mr_song_shards(ctypes.byref(cd), n_shards, b.ctypes.data_as(ctypes.c_void_p)), "mr_song_shards")
+    if tile > 0:
+        _lib.check(L.mr_song_shards_tiled(ctypes.byref(cd), n_shards, int(tile), b.ctypes.data_as(ctypes.c_void_p)),
+                   "mr_song_shards_tiled")
+    else:
+        _lib.check(L.mr_song_shards(ctypes.byref(cd), n_shards, b.ctypes.data_as(ctypes.c_void_p)),
+                   "mr_song_shards")
     return [(int(b[g]), int(b[g + 1])) for g in range(n_shards)]
 
 

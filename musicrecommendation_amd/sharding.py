@@ -28,8 +28,12 @@ import numpy as np
 from .dataset import Dataset
 
 
-def song_shards(ds: Dataset, n_shards: int) -> List[Tuple[int, int]]:
-    """[lo, hi) song ranges with ~equal Σ (c_tr(s) + 1)."""
+def song_shards(ds: Dataset, n_shards: int, tile: int = 0) -> List[Tuple[int, int]]:
+    """[lo, hi) song ranges with ~equal Σ (c_tr(s) + 1). tile > 0: then every
+    boundary moves the least so that no shard is wider than
+    ceil(ceil(n_songs / tile) / n_shards) tiles (mr_song_shards_tiled; the
+    wide kernel walks a test user's neighbour list once per tile, so a shard a
+    few songs past whole tiles pays a whole extra tile)."""
     if n_shards < 1:
         raise ValueError("n_shards must be >= 1")
     c_tr = np.bincount(ds.tr_songs, minlength=ds.n_songs).astype(np.int64)
@@ -40,7 +44,37 @@ def song_shards(ds: Dataset, n_shards: int) -> List[Tuple[int, int]]:
         b = int(np.searchsorted(cost, total * g / n_shards, side="left")) + 1
         bounds.append(min(max(b, bounds[-1] + 1), ds.n_songs - (n_shards - g)))
     bounds.append(ds.n_songs)
+    if tile > 0:
+        n_s = ds.n_songs
+        tiles = (n_s + tile - 1) // tile
+        cap = (tiles + n_shards - 1) // n_shards * tile  # songs per shard at most
+        for g in range(1, n_shards):
+            x = max(bounds[g], n_s - (n_shards - g) * cap)
+            x = min(x, bounds[g - 1] + cap)
+            x = max(x, bounds[g - 1] + 1)
+            bounds[g] = min(x, n_s - (n_shards - g))
     return [(bounds[g], bounds[g + 1]) for g in range(n_shards)]
+
+
+def shard_tile(n_train: int, n_test: int, *, topk: int = 10, stage1: str = "auto", block_songs: int = 0,
+               stage1_chunk: int = 0) -> int:
+    """The wide shape's song tile for a context scoring n_test x n_train users
+    with these options (mr_shard_tile_songs), 0 when it would use another shape."""
+    import ctypes
+
+    from . import _lib
+
+    L = _lib.lib()
+    opt = _lib.MrOptions()
+    _lib.check(L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
+    opt.topk = topk
+    opt.block_songs = block_songs
+    opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4, "user": 5}[stage1]
+    opt.stage1_chunk = stage1_chunk
+    out = ctypes.c_int32()
+    _lib.check(L.mr_shard_tile_songs(ctypes.byref(opt), int(n_train), int(n_test), ctypes.byref(out)),
+               "mr_shard_tile_songs")
+    return out.value
 
 
 def user_blocks(n_test: int, n_blocks: int) -> List[Tuple[int, int]]:
@@ -130,7 +164,8 @@ class ShardScorer:
         self.rank, self.world = rank, world
         self.block, self.shard = rank // self.gs, rank % self.gs
         self.user_lo, self.user_hi = user_blocks(ds.n_test, self.gu)[self.block]
-        self.song_lo, self.song_hi = song_shards(ds, self.gs)[self.shard]
+        tile = shard_tile(ds.n_train, ds.n_test // self.gu, topk=topk, stage1=stage1, block_songs=block_songs)
+        self.song_lo, self.song_hi = song_shards(ds, self.gs, tile)[self.shard]
         self.full = ds
         self.ds = ds if self.gu == 1 else ds.subset_test_users(self.user_lo, self.user_hi)
         self.group = block_group(rank, world, self.gs) if world > 1 else None

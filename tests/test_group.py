@@ -1,7 +1,8 @@
 """Multi-GPU behind the C ABI (mr_group_*, the reference's getItemBasedModel2 /
 getUserBasedModel2 fan-out, distributed.scala:459-479).
 
-CPU: the shard boundaries of the library (mr_song_shards) equal
+CPU: the shard boundaries of the library (mr_song_shards, and
+mr_song_shards_tiled: no shard past the fewest whole wide tiles) equal
 sharding.song_shards (Σ(c_tr + 1) balance); creating a group without a GPU
 fails with an error code (never a crash or a CPU fallback).
 GPU (one MI355X): G = song shards x user blocks logical contexts on device 0
@@ -16,7 +17,7 @@ import pytest
 
 from musicrecommendation_amd import _lib, synth
 from musicrecommendation_amd.group import Group, song_shards_native
-from musicrecommendation_amd.sharding import song_shards
+from musicrecommendation_amd.sharding import shard_tile, song_shards
 
 from helpers import kat, dataset_from_lines, synth_fixture
 
@@ -32,6 +33,38 @@ def test_native_song_shards_equal_python_rule():
     for name, ds in _datasets():
         for n in range(1, min(9, ds.n_songs) + 1):
             assert song_shards_native(ds, n) == song_shards(ds, n), (name, n)
+
+
+def test_tiled_song_shards():
+    """mr_song_shards_tiled = sharding.song_shards(..., tile): no shard wider
+    than ceil(ceil(n_songs / tile) / n) tiles, boundaries otherwise the
+    balanced ones; tile 0 = the plain balance."""
+    for name, ds in _datasets():
+        for n in range(1, min(9, ds.n_songs) + 1):
+            assert song_shards_native(ds, n, 0) == song_shards(ds, n), (name, n)
+            for tile in (1, 3, 7, 64, 256, 1000):
+                got = song_shards(ds, n, tile)
+                assert song_shards_native(ds, n, tile) == got, (name, n, tile)
+                assert got[0][0] == 0 and got[-1][1] == ds.n_songs
+                assert all(hi > lo for lo, hi in got) and all(a[1] == b[0] for a, b in zip(got, got[1:]))
+                tiles = -(-ds.n_songs // tile)
+                cap = -(-tiles // n) * tile  # songs per shard at most
+                assert max(hi - lo for lo, hi in got) <= cap, (name, n, tile)
+                if tile >= ds.n_songs:  # one tile holds every shard: the balance is kept
+                    assert got == song_shards(ds, n)
+
+
+def test_shard_tile_follows_the_shape_rule():
+    # C4-sized train set: wide, the widest tile the LDS holds (k = 10)
+    assert shard_tile(1_009_318, 10_000) == 19_456
+    assert shard_tile(1_009_318, 10_000, block_songs=8192) == 8192
+    # C2 (500 x 10): fused, no wide tile; forced wide: the widest tile
+    assert shard_tile(500, 10) == 0
+    assert shard_tile(500, 10, stage1="wide") == 19_456
+    # k > 16 never takes the wide shape
+    assert shard_tile(1_009_318, 10_000, topk=17) == 0
+    with pytest.raises(_lib.EngineError):
+        shard_tile(10, 0)
 
 
 def test_group_without_gpu_fails_cleanly():
@@ -61,7 +94,7 @@ def test_copy_group_equals_one_context(layout):
                 ref[model] = (e.dense(), *e.topk())
         with Group(ds, song_shards=gs, user_blocks=gu, out_dtype="f64", topk=7) as g:
             assert g.transport == "copy" and len(g.layout) == gs * gu
-            shards = song_shards(ds, gs)
+            shards = song_shards(ds, gs, shard_tile(ds.n_train, ds.n_test // gu, topk=7))
             for i, (slo, shi, ulo, uhi, dev) in enumerate(g.layout):
                 assert (slo, shi) == shards[i % gs] and dev == 0
             for model in ("ibm", "ubm"):
@@ -152,7 +185,7 @@ def test_c3_song_sharded_group_equals_one_context():
             e.run(model)
             ref[model] = (e.dense(), e.topk()[0], e.topk()[2])
     with Group(ds, song_shards=2, out_dtype="f32", topk=10) as g:
-        assert [(lo, hi) for lo, hi, *_ in g.layout] == song_shards(ds, 2)
+        assert [(lo, hi) for lo, hi, *_ in g.layout] == song_shards(ds, 2, shard_tile(ds.n_train, ds.n_test))
         for model in ("ubm", "ibm"):
             g.run(model)
             songs, _scores, keys = g.topk()
@@ -164,6 +197,22 @@ def test_c3_song_sharded_group_equals_one_context():
             for b in bufs:
                 assert np.array_equal(b.cpu().numpy(), d_ref, equal_nan=True), model
             del bufs
+
+
+@pytest.mark.gpu
+def test_shard_tile_matches_the_loaded_contexts():
+    """mr_shard_tile_songs (host, before any load) is the tile the loaded
+    contexts use: every tiled shard of C3 holds ceil(width / tile) tiles."""
+    from musicrecommendation_amd.engine import Engine
+
+    ds = synth.config("c3").dataset()
+    tile = shard_tile(ds.n_train, ds.n_test)
+    assert tile > 0
+    for gs in (2, 3, 5):
+        for lo, hi in song_shards(ds, gs, tile):
+            with Engine(ds, topk=10, dense=False, song_lo=lo, song_hi=hi) as e:
+                assert e.shape == "wide" and e.block_songs <= tile
+                assert e.n_tiles == -(-(hi - lo) // tile), (gs, lo, hi)
 
 
 @pytest.mark.gpu
