@@ -411,6 +411,12 @@ int mr_corpus_labels(const mr_corpus* c, const int64_t** off, const int32_t** so
 /* String ids (NUL-terminated, owned by the corpus). kind: 0 = song (ids
  * 0..n_songs+n_extra_songs), 1 = train user, 2 = test user. */
 const char* mr_corpus_name(const mr_corpus* c, int32_t kind, int32_t id);
+/* Every name of `kind` in id order, each followed by '\n' (names hold no tab or
+ * newline: they are TSV fields), into buf[0..buf_size); *bytes_needed = the
+ * total. buf = NULL (or too small): only *bytes_needed is set (and
+ * MR_E_INVALID returned when buf is non-NULL). One call instead of one per
+ * name: 1.4M names at full scale. */
+int mr_corpus_names(const mr_corpus* c, int32_t kind, char* buf, int64_t buf_size, int64_t* bytes_needed);
 int mr_corpus_free(mr_corpus* c);
 
 /* ---- model files (MR:489-512) --------------------------------------------

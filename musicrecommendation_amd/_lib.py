@@ -160,6 +160,7 @@ SIGNATURES = {
     "mr_corpus_dataset": (c_int, [c_void_p, POINTER(MrDataset)]),
     "mr_corpus_labels": (c_int, [c_void_p, POINTER(POINTER(c_int64)), POINTER(POINTER(c_int32)), POINTER(c_int32), POINTER(c_int32)]),
     "mr_corpus_name": (c_char_p, [c_void_p, c_int32, c_int32]),
+    "mr_corpus_names": (c_int, [c_void_p, c_int32, c_char_p, c_int64, POINTER(c_int64)]),
     "mr_corpus_free": (c_int, [c_void_p]),
     "mr_version": (c_char_p, []),
     "mr_model_write_tsv": (c_int, [c_char_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_int32]),

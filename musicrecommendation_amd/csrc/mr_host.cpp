@@ -308,6 +308,25 @@ const char* mr_corpus_name(const mr_corpus* c, int32_t kind, int32_t id) {
   return (*v)[id].c_str();
 }
 
+int mr_corpus_names(const mr_corpus* c, int32_t kind, char* buf, int64_t buf_size, int64_t* bytes_needed) {
+  if (!c || !bytes_needed) return mr_host::fail(MR_E_INVALID, "null argument");
+  const std::vector<std::string>* v =
+      kind == 0 ? &c->song_names : kind == 1 ? &c->train_names : kind == 2 ? &c->test_names : nullptr;
+  if (!v) return mr_host::fail(MR_E_INVALID, "bad name kind %d", kind);
+  int64_t total = 0;
+  for (const auto& s : *v) total += (int64_t)s.size() + 1;
+  *bytes_needed = total;
+  if (!buf) return MR_OK;
+  if (buf_size < total) return mr_host::fail(MR_E_INVALID, "name buffer of %lld B, %lld needed", (long long)buf_size, (long long)total);
+  char* o = buf;
+  for (const auto& s : *v) {
+    std::memcpy(o, s.data(), s.size());
+    o += s.size();
+    *o++ = '\n';
+  }
+  return MR_OK;
+}
+
 int mr_corpus_free(mr_corpus* c) {
   delete c;
   return MR_OK;

@@ -145,9 +145,19 @@ class Dataset:
             _lib.check(L.mr_corpus_labels(h, ctypes.byref(lo), ctypes.byref(ls), ctypes.byref(nl), ctypes.byref(ne)),
                        "mr_corpus_labels")
             lab_off = arr(lo, n_te + 1, np.int64)
-            names_s = [L.mr_corpus_name(h, 0, i).decode() for i in range(n_s + ne.value)]
-            names_tr = [L.mr_corpus_name(h, 1, i).decode() for i in range(n_tr)]
-            names_te = [L.mr_corpus_name(h, 2, i).decode() for i in range(n_te)]
+            def names(kind, n):  # one bulk copy per kind (mr_corpus_names)
+                need = ctypes.c_int64()
+                _lib.check(L.mr_corpus_names(h, kind, None, 0, ctypes.byref(need)), "mr_corpus_names")
+                buf = ctypes.create_string_buffer(max(1, need.value))
+                _lib.check(L.mr_corpus_names(h, kind, buf, need.value, ctypes.byref(need)), "mr_corpus_names")
+                out = buf.raw[:need.value].decode().split("\n")[:-1]
+                if len(out) != n:
+                    raise RuntimeError(f"mr_corpus_names: {len(out)} names of kind {kind}, expected {n}")
+                return out
+
+            names_s = names(0, n_s + ne.value)
+            names_tr = names(1, n_tr)
+            names_te = names(2, n_te)
             return Dataset(
                 n_train=n_tr, n_test=n_te, n_songs=n_s,
                 tr_off=tr_off, tr_songs=arr(d.tr_songs, int(tr_off[-1]), np.int32),

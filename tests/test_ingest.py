@@ -115,3 +115,27 @@ def test_parallel_chunks_identical(tmp_path, monkeypatch, threads):
     with pytest.raises(_lib.EngineError) as ei:
         Dataset.from_tsv(*paths)
     assert ei.value.code == _lib.MR_E_PARSE and f":{len(lines) // 2 + 1}:" in str(ei.value)
+
+
+def test_bulk_names_errors_and_empty_names(tmp_path):
+    """mr_corpus_names: every name in id order, each followed by a newline
+    (empty names included); bad kind / short buffer are error codes."""
+    import ctypes
+
+    (tmp_path / "tr.txt").write_text("u1\ts2\t1\nu0\ts1\t1\n\ts1\t1\n")  # an empty user name (Java split keeps it)
+    (tmp_path / "te.txt").write_text("t0\ts2\t1\n")
+    ds = Dataset.from_tsv(str(tmp_path / "tr.txt"), str(tmp_path / "te.txt"))
+    assert [ds.train_names(i) for i in range(ds.n_train)] == ["", "u0", "u1"]
+    assert [ds.song_names(i) for i in range(ds.n_songs)] == ["s1", "s2"]
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.mr_corpus_from_tsv(os.fsencode(str(tmp_path / "tr.txt")), os.fsencode(str(tmp_path / "te.txt")),
+                                    None, ctypes.byref(h)), "mr_corpus_from_tsv")
+    try:
+        need = ctypes.c_int64()
+        assert L.mr_corpus_names(h, 1, None, 0, ctypes.byref(need)) == 0 and need.value == len("\nu0\nu1\n")
+        small = ctypes.create_string_buffer(2)
+        assert L.mr_corpus_names(h, 1, small, 2, ctypes.byref(need)) == _lib.MR_E_INVALID
+        assert L.mr_corpus_names(h, 7, None, 0, ctypes.byref(need)) == _lib.MR_E_INVALID
+    finally:
+        L.mr_corpus_free(h)
