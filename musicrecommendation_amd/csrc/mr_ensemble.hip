@@ -244,14 +244,15 @@ __global__ __launch_bounds__(kThreads) void k_eval_tp(EvalParams p) {
   for (int t = 0; t < c; ++t) atomicAdd(&p.tp[(size_t)g * kThresholds + t], 1);
 }
 
-// AP of every song class of the shard (MR:588-618), the host fold's exact
-// double operations (mr_eval_map) per class; classes nobody holds get 0.
-__global__ __launch_bounds__(kThreads) void k_eval_ap(int width, int song_lo, const int* pred, const int* tp,
-                                                      const int* pos, double* ap) {
-  const int g = blockIdx.x * kThreads + threadIdx.x;
-  if (g >= width) return;
-  const int np = pos[g];
-  if (np <= 0) { ap[g] = 0.0; return; }
+// AP of the label classes cls[0..n) of the shard (shard-local song ids, np =
+// their label counts pos, all > 0; MR:588-618), the host fold's exact double
+// operations (mr_eval_map) per class.
+__global__ __launch_bounds__(kThreads) void k_eval_ap(int n, const int* cls, const int* cpos, const int* pred,
+                                                      const int* tp, double* ap) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= n) return;
+  const int g = cls[c];
+  const int np = cpos[c];
   double P[kThresholds], R[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) {
@@ -265,8 +266,7 @@ __global__ __launch_bounds__(kThreads) void k_eval_ap(int width, int song_lo, co
     const double term = t == 9 ? 0.0 : t == 8 ? (R[8] - 0.0) * P[8] : (R[t] - R[t + 1]) * P[t];
     a = a + term;
   }
-  ap[g] = a;
-  (void)song_lo;
+  ap[c] = a;
 }
 
 template <typename T>
@@ -381,9 +381,10 @@ int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx
   MR_HIP(hipSetDevice(v.device));
   const long long n = (long long)v.n_test_users * (v.song_hi - v.song_lo);
   const int blocks = (int)std::max<long long>(1, std::min<long long>(4096, (n + kThreads - 1) / kThreads));
-  Tmp<double> part;
-  MR_HIP(hipMalloc(reinterpret_cast<void**>(&part.p), (size_t)blocks * 2 * sizeof(double)));
   hipStream_t st = (hipStream_t)v.stream;
+  Tmp<double> part;
+  part.st = st;
+  MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&part.p), (size_t)blocks * 2 * sizeof(double), st));
   if (v.out_dtype == MR_OUT_F64)
     hipLaunchKernelGGL(k_minmax<double>, dim3(blocks), dim3(kThreads), 0, st, (const double*)dense, n, part.p);
   else
@@ -426,23 +427,30 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
   if (rc) return rc;
   hipStream_t st = (hipStream_t)v.stream;
   const int width = v.song_hi - v.song_lo;
-  Tmp<int> d_pos;
-  Tmp<double> d_ap;
-  d_pos.st = d_ap.st = st;
-  std::vector<double> ap((size_t)std::max(1, width));
-  if (width > 0) {
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_pos.p), (size_t)width * 4, st));
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)width * 8, st));
-    MR_HIP(hipMemcpyAsync(d_pos.p, pos + v.song_lo, (size_t)width * 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_eval_ap, dim3((width + kThreads - 1) / kThreads), dim3(kThreads), 0, st, width, v.song_lo,
-                       d_pred.p, d_tp.p, d_pos.p, d_ap.p);
-    MR_HIP(hipGetLastError());
-    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)width * 8, hipMemcpyDeviceToHost, st));
-    MR_HIP(hipStreamSynchronize(st));
-  }
-  double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
+  // Only the label classes (pos > 0, ascending) cross PCIe: their ids and
+  // counts in, their AP out (C5: ~1/10 of the shard's songs).
+  std::vector<int32_t> cls, cpos;
   for (int g = 0; g < width; ++g)
-    if (pos[v.song_lo + g] > 0) total += ap[g];
+    if (pos[v.song_lo + g] > 0) { cls.push_back(g); cpos.push_back(pos[v.song_lo + g]); }
+  const int nc = (int)cls.size();
+  Tmp<int> d_cls, d_cpos;
+  Tmp<double> d_ap;
+  d_cls.st = d_cpos.st = d_ap.st = st;
+  std::vector<double> ap((size_t)std::max(1, nc));
+  if (nc > 0) {
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)nc * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cpos.p), (size_t)nc * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)nc * 8, st));
+    MR_HIP(hipMemcpyAsync(d_cls.p, cls.data(), (size_t)nc * 4, hipMemcpyHostToDevice, st));
+    MR_HIP(hipMemcpyAsync(d_cpos.p, cpos.data(), (size_t)nc * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_eval_ap, dim3((nc + kThreads - 1) / kThreads), dim3(kThreads), 0, st, nc, d_cls.p,
+                       d_cpos.p, d_pred.p, d_tp.p, d_ap.p);
+    MR_HIP(hipGetLastError());
+    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)nc * 8, hipMemcpyDeviceToHost, st));
+  }
+  MR_HIP(hipStreamSynchronize(st));
+  double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
+  for (int c = 0; c < nc; ++c) total += ap[c];
   *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
   return MR_OK;
 }
