@@ -542,12 +542,34 @@ __device__ __forceinline__ void thread_best(int n, Get get, long long& mk, int& 
     if (key >= 0) take_if_before(mk, ms, key, song);
   }
 }
+// A top-k list's global destination: key / song (and score = the key's
+// double, NaN for none, when non-null), written by the thread that ranked the
+// slot — sc1 stores for an in-launch hand-off — instead of through LDS; the
+// caller orders the stores (no barrier after them). key == nullptr: LDS out.
+struct TopkDst {
+  long long* key = nullptr;
+  int* song = nullptr;
+  double* score = nullptr;
+  bool sc1 = false;
+};
+__device__ __forceinline__ void topk_dst_write(const TopkDst& d, int slot, long long key, int song) {
+  if (d.sc1) {
+    __hip_atomic_store(d.key + slot, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.song + slot, song, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    d.key[slot] = key;
+    d.song[slot] = song;
+  }
+  if (d.score) d.score[slot] = key >= 0 ? __longlong_as_double(key) : (double)NAN;
+}
+
 // Ranks of nc <= 256 survivor candidates ck/cs among themselves (total order
 // (key desc, song asc)): rank < k -> output slot; slots past nc get (-1, -1).
-// crank: 256 zeroed ints. All threads call it; it ends with a barrier.
+// crank: 256 zeroed ints. All threads call it; it ends with a barrier (not
+// after the stores to a global dst).
 template <int NT>
 __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* ck, const int* cs, int* crank,
-                                               long long* out_k, int* out_s) {
+                                               long long* out_k, int* out_s, const TopkDst& dst = TopkDst{}) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (nc * nc > 16 * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
     if (tid < 64) {
@@ -562,6 +584,8 @@ __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* c
       wave_topk_regs<4>(rk, rs, k, out_k, out_s);
     }
     __syncthreads();
+    if (dst.key)
+      for (int r = tid; r < k; r += NT) topk_dst_write(dst, r, out_k[r], out_s[r]);
     return;
   }
   if (nc > 0) {  // candidate ranks: nc x nc comparisons, <= 16 per thread
@@ -577,6 +601,11 @@ __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* c
     }
   }
   __syncthreads();
+  if (dst.key) {
+    if (tid < nc && crank[tid] < k) topk_dst_write(dst, crank[tid], ck[tid], cs[tid]);
+    if (tid >= nc && tid < k) topk_dst_write(dst, tid, kKeyNone, -1);  // fewer than k entries
+    return;
+  }
   if (tid < nc && crank[tid] < k) { out_k[crank[tid]] = ck[tid]; out_s[crank[tid]] = cs[tid]; }
   if (tid >= nc && tid < k) { out_k[tid] = kKeyNone; out_s[tid] = -1; }  // fewer than k entries
   __syncthreads();
@@ -588,7 +617,7 @@ __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* c
 template <int NT, typename Get, int NG = NT / 16>
 __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long long mk, int ms, unsigned char* gm,
                                                      long long* ck, int* cs, int cap, long long* out_k, int* out_s,
-                                                     long long* sb = nullptr) {
+                                                     long long* sb = nullptr, const TopkDst& dst = TopkDst{}) {
   constexpr int GS = NT / NG;  // threads per row
   static_assert(NT % 64 == 0 && NT % NG == 0 && NG <= 64 && GS <= 64 && NT * 16 >= NG * NG,
                 "block shape");
@@ -658,7 +687,7 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   stamp_at(sb, 11);
   const int nc = *counter;
   if (nc > cap) return false;
-  rank_survivors<NT>(nc, k, ck, cs, crank, out_k, out_s);
+  rank_survivors<NT>(nc, k, ck, cs, crank, out_k, out_s, dst);
   return true;
 }
 
@@ -1247,6 +1276,23 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     song = blo + i;
   };
   bool thr_done = false;  // threshold pass first (about k candidates, ranked in parallel)
+  // The tile's list goes straight from the ranking threads to its global
+  // slots (sc1 for the hand-off; the user's outputs when the tile is the
+  // whole shard), not through LDS + a barrier + a copy loop.
+  long long* ck = p.cand_key + (size_t)u * p.n_tiles * k;
+  int* cs = p.cand_song + (size_t)u * p.n_tiles * k;
+  TopkDst tdst;
+#ifndef MR_TOPK_VIA_LDS
+  if (p.n_tiles == 1) {
+    tdst.key = p.top_key + (size_t)u * k;
+    tdst.song = p.top_song + (size_t)u * k;
+    tdst.score = p.top_score + (size_t)u * k;
+  } else {
+    tdst.key = ck + (size_t)tile * k;
+    tdst.song = cs + (size_t)tile * k;
+    tdst.sc1 = true;
+  }
+#endif
   if (!p.topk_lists && k <= kThreads / 16) {
 #ifdef MR_STAMPS
     long long* sbt = sb ? sb + 3 : nullptr;  // sub-phase stamps in slots 12-14
@@ -1254,8 +1300,9 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     long long* sbt = nullptr;
 #endif
     thr_done = block_topk_threshold<kThreads, decltype(get_key), MR_TILE_ROWS>(
-        bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK, fk, fs, sbt);
+        bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK, fk, fs, sbt, tdst);
   }
+  const bool direct = thr_done && tdst.key;
   if (thr_done) {
   } else if (bs <= kMaxTopkTile) {
     block_topk(bw, k, get_key, wk, ws, fk, fs);
@@ -1267,12 +1314,13 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   MR_STAMP(4);
 
   if (p.n_tiles == 1) {  // the tile is the whole shard: publish directly
-    for (int r = tid; r < k; r += kThreads) {
-      const size_t o = (size_t)u * k + r;
-      p.top_key[o] = fk[r];
-      p.top_song[o] = fs[r];
-      p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
-    }
+    if (!direct)
+      for (int r = tid; r < k; r += kThreads) {
+        const size_t o = (size_t)u * k + r;
+        p.top_key[o] = fk[r];
+        p.top_song[o] = fs[r];
+        p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+      }
     return;
   }
 
@@ -1287,12 +1335,11 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   // scope would lower to buffer_wbl2 sc1 + buffer_inv sc1 — a write-back of
   // the XCD's whole L2 (≈1.7-6.5 us per the guide's price table) on every
   // tile's critical path — and adds nothing this protocol needs on gfx950.
-  long long* ck = p.cand_key + (size_t)u * p.n_tiles * k;
-  int* cs = p.cand_song + (size_t)u * p.n_tiles * k;
-  for (int r = tid; r < k; r += kThreads) {
-    st_sc1(&ck[(size_t)tile * k + r], fk[r]);
-    st_sc1(&cs[(size_t)tile * k + r], fs[r]);
-  }
+  if (!direct)
+    for (int r = tid; r < k; r += kThreads) {
+      st_sc1(&ck[(size_t)tile * k + r], fk[r]);
+      st_sc1(&cs[(size_t)tile * k + r], fs[r]);
+    }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -1307,6 +1354,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
 #endif
   if (!*flag) return;
 
+  bool merged_direct = false;  // the merge's select wrote the user's outputs itself
   // Last tile of user u: tournament over the tiles' sorted candidate lists,
   // staged into LDS region A with sc1 loads (stage_lists lists per pass; the
   // running top-k is list 0 of every later pass). (A prune-by-max-k-th-key +
@@ -1317,6 +1365,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     int* ms = reinterpret_cast<int*>(smem_raw + L.acc + L.stage_lists * k * 8);
     const int w = tid >> 6;
     int done = 0, off = 0;
+    merged_direct = false;
     while (done < p.n_tiles) {
       const int nl = min(p.n_tiles - done, L.stage_lists - off);
       // 4 candidates per thread in flight per batch (loads first, then LDS)
@@ -1349,6 +1398,12 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       __syncthreads();
       MR_STAMP(6);
       bool merged = false;
+      TopkDst mdst;  // the user's outputs, written by the ranking threads
+#ifndef MR_TOPK_VIA_LDS
+      mdst.key = p.top_key + (size_t)u * k;
+      mdst.song = p.top_song + (size_t)u * k;
+      mdst.score = p.top_score + (size_t)u * k;
+#endif
       // (A threshold on the sorted lists' HEADS — the k-th best head — measured
       // 16.7 vs 14.0 us per C2 step: it is a much looser bound than the row
       // bests, ~5x the survivors to rank; profiles/r02/c2_merge_heads_ab.txt.)
@@ -1359,29 +1414,31 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         thread_best<kThreads>(nl * k, get_c, bk, bsg);
         if (p.merge_rows == 16)
           merged = block_topk_threshold<kThreads, decltype(get_c), 16>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
-                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs, nullptr, mdst);
         else if (p.merge_rows == 64)
           merged = block_topk_threshold<kThreads, decltype(get_c), 64>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
-                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs, nullptr, mdst);
         else
           merged = block_topk_threshold<kThreads, decltype(get_c), 32>(nl * k, k, get_c, bk, bsg, smem_raw + L.gm,
-                                                                      wk, ws, kWaves * kMaxTopK, fk, fs);
+                                                                      wk, ws, kWaves * kMaxTopK, fk, fs, nullptr, mdst);
       }
       if (!merged) {
         if (w == 0) wave_merge_lists(nl + off, k, mk, ms, fk, fs);
         __syncthreads();
       }
       MR_STAMP(8);
+      merged_direct = merged && mdst.key;
       done += nl;
       off = 1;
     }
   }
-  for (int r = tid; r < k; r += kThreads) {
-    const size_t o = (size_t)u * k + r;
-    p.top_key[o] = fk[r];
-    p.top_song[o] = fs[r];
-    p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
-  }
+  if (!merged_direct)
+    for (int r = tid; r < k; r += kThreads) {
+      const size_t o = (size_t)u * k + r;
+      p.top_key[o] = fk[r];
+      p.top_song[o] = fs[r];
+      p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+    }
   if (tid == 0) p.counter[u] = 0u;  // ready for the next launch (kernel boundary orders it)
   MR_STAMP(9);
 }
