@@ -1366,7 +1366,31 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     const int w = tid >> 6;
     int done = 0, off = 0;
     merged_direct = false;
-    while (done < p.n_tiles) {
+#ifndef MR_MERGE_VIA_LDS
+    // At most one candidate per thread (C2: 22 tiles x 10 <= 256): each thread
+    // loads its candidate into registers and the threshold select reads it
+    // there — no LDS staging pass and barrier before the select.
+    const int nck = p.n_tiles * k;
+    if (!p.topk_lists && nck <= kThreads && k <= kThreads / 16 && p.merge_rows == 32) {
+      long long rk = kKeyNone;
+      int rs = INT_MAX;
+      if (tid < nck) {
+        rk = ld_sc1(&ck[tid]);
+        rs = ld_sc1(&cs[tid]);
+      }
+      MR_STAMP(6);
+      auto get_r = [&](int, long long& key, int& song) { key = rk; song = rs; };  // called for i = tid only
+      TopkDst mdst;
+      mdst.key = p.top_key + (size_t)u * k;
+      mdst.song = p.top_song + (size_t)u * k;
+      mdst.score = p.top_score + (size_t)u * k;
+      merged_direct = block_topk_threshold<kThreads, decltype(get_r), 32>(
+          nck, k, get_r, rk >= 0 ? rk : kKeyNone, rk >= 0 ? rs : INT_MAX, smem_raw + L.gm, wk, ws,
+          kWaves * kMaxTopK, fk, fs, nullptr, mdst);
+      MR_STAMP(8);
+    }
+#endif
+    while (!merged_direct && done < p.n_tiles) {
       const int nl = min(p.n_tiles - done, L.stage_lists - off);
       // 4 candidates per thread in flight per batch (loads first, then LDS)
       for (int i0 = tid; i0 < nl * k; i0 += 4 * kThreads) {
