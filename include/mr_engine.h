@@ -101,7 +101,7 @@ typedef struct mr_options {
   int32_t frac_bits;   /* fixed-point fraction bits F of the int64 accumulators (default 32, 8..40) */
   int32_t song_lo;     /* first song id of this context's shard (default 0) */
   int32_t song_hi;     /* one past the last song id; <= 0 means n_songs (default 0) */
-  int32_t block_songs; /* songs per LDS accumulator tile (pull shape: songs per range); 0 = auto
+  int32_t block_songs; /* songs per LDS accumulator tile; 0 = auto
                           (multiple of 256, <= 16384) */
   int32_t out_dtype;   /* MR_OUT_F32 (default) or MR_OUT_F64 for the dense model */
   int32_t topk;        /* k of the per-test-user recommendation list (0 = off, <= 64; default 10) */
@@ -110,21 +110,17 @@ typedef struct mr_options {
                           perturb back-to-back launches — see mr_kernel_times / mr_timing_begin) */
   int32_t stage1;      /* launch shape: 0 = auto, 1 = fused (one kernel; stage 1 recomputed per
                           song tile in LDS; n_train_users <= 4096), 2 = separate stage-1 kernel
-                          (compact neighbour lists), 3 = pull (stage 1 writes a dense
-                          Yt[train user][test user] slab, the scoring kernel gathers its rows per
-                          song; topk <= 16), 4 = wide (large train sets: chunked stage 1, 16k-song
-                          tiles scored by 1024-thread workgroups, separate top-k merge launch;
-                          topk <= 16), 5 = user (one 1024-thread workgroup per test user scores
-                          the whole shard in one LDS tile, stage 1 fused; small catalogues:
-                          shard x 8 B + n_train_users x 8 B within the 160 KiB LDS; topk <= 16).
-                          Auto (topk <= 16): wide when n_train_users > 4096 or n_test_users x
-                          n_train_users >= 1e5, else fused; topk > 16: fused when
-                          n_train_users <= 4096, else separate. Pull and user on request. */
+                          (compact neighbour lists), 4 = wide (large train sets: chunked stage 1,
+                          16k-song tiles scored by 1024-thread workgroups, separate top-k merge
+                          launch; topk <= 16). (3 and 5 named round-2 shapes that were never
+                          faster and are gone: MR_E_INVALID.) Auto (topk <= 16): wide when
+                          n_train_users > 4096 or n_test_users x n_train_users >= 1e5, else
+                          fused; topk > 16: fused when n_train_users <= 4096, else separate. */
   int32_t stage1_chunk;/* separate shape: train users per stage-1 LDS chunk; 0 = auto (all of them up
                           to 16384, else 4096); smaller values exercise the chunked path */
   int32_t train_order; /* 0 (default) = train users renumbered internally by distinct-song count
                           (descending) for load balance; 1 = as given. Results are identical. */
-  int32_t topk_lists;  /* 1 = tile top-k of the wide / user shapes by per-thread running lists only
+  int32_t topk_lists;  /* 1 = tile top-k of the wide shape by per-thread running lists only
                           (diagnostic); 0 (default) = a threshold pass first (about k candidates),
                           the lists only when ties overflow it. Results are identical. */
   int32_t reserved[3];
@@ -146,10 +142,9 @@ int mr_load(mr_ctx* ctx, const mr_dataset* d);
  * test users. The dense model of this context is n_te x (song_hi - song_lo). */
 int mr_shard_info(const mr_ctx* ctx, int32_t* song_lo, int32_t* song_hi, int32_t* n_test_users);
 
-/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 2 pull, 3 wide,
- * 4 user (auto picks fused or wide for topk <= 16, fused or separate above;
- * pull and user only on request, see mr_options.stage1); songs per LDS tile
- * (pull: per song range) and tiles (ranges) per test user. */
+/* Launch shape chosen by mr_load: *shape = 0 separate, 1 fused, 3 wide (auto
+ * picks fused or wide for topk <= 16, fused or separate above; see
+ * mr_options.stage1); songs per LDS tile and tiles per test user. */
 int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int32_t* n_tiles);
 
 /* Test-user batch of the separate / wide shapes (mr_run launches the stage-1 and
@@ -287,8 +282,8 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
                        const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
- * (0 = separate stage-1 kernel — neighbour lists or pull columns —, 1 = the
- * scoring kernels — stage 2, fused stage 1, the in-launch top-k merge, the pull
+ * (0 = separate stage-1 kernel — neighbour lists —, 1 = the
+ * scoring kernels — stage 2, fused stage 1, the in-launch top-k merge, the wide
  * kernel and its top-k merge —, 2 = reserved) the number of
  * timed launches and their summed device milliseconds; reset=1 clears. */
 int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total_ms, int32_t reset);
@@ -304,11 +299,6 @@ int mr_timing_end(mr_ctx* ctx, int64_t* launches, double* total_ms);
  * per-workgroup phase timestamps of the last scoring launch ([grid][8]
  * s_memrealtime values); MR_E_STATE in the production build. */
 int mr_debug_stamps(mr_ctx* ctx, int64_t* out, int64_t n);
-
-/* Diagnostic builds only (libmr_engine_checks.so, -DMR_CHECKS): bits of the
- * array classes whose index went out of range in the pull-shape kernels since
- * mr_load (0 = none); MR_E_STATE in the production build. */
-int mr_debug_checks(mr_ctx* ctx, uint32_t* bits);
 
 /* HIP stream of the context (as void* = hipStream_t). */
 void* mr_stream(const mr_ctx* ctx);

@@ -15,8 +15,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MR_ENGINE_LIB=stamps|checks selects a diagnostic build (phase timestamps /
-# bounds-checked pull kernels).
+# MR_ENGINE_LIB=stamps selects the diagnostic build (per-workgroup phase timestamps).
 _VARIANT = os.environ.get("MR_ENGINE_LIB", "")
 LIB_PATH = os.path.join(_HERE, f"libmr_engine_{_VARIANT}.so" if _VARIANT else "libmr_engine.so")
 
@@ -31,6 +30,9 @@ MR_E_RCCL = -7
 MR_TRANSPORT_AUTO, MR_TRANSPORT_COPY, MR_TRANSPORT_RCCL = 0, 1, 2
 MR_UBM = 0
 MR_IBM = 1
+# mr_options.stage1 by name, and mr_launch_info's shape codes
+STAGE1 = {"auto": 0, "fused": 1, "separate": 2, "wide": 4}
+SHAPES = {0: "separate", 1: "fused", 3: "wide"}
 MR_OUT_F32 = 0
 MR_OUT_F64 = 1
 
@@ -142,7 +144,6 @@ SIGNATURES = {
     "mr_topk_merge_device": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),
     "mr_debug_stamps": (c_int, [c_void_p, c_void_p, c_int64]),
-    "mr_debug_checks": (c_int, [c_void_p, c_void_p]),
     "mr_timing_begin": (c_int, [c_void_p]),
     "mr_timing_end": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double)]),
     "mr_stream": (c_void_p, [c_void_p]),

@@ -40,7 +40,6 @@ def _stale(out: str = OUT) -> bool:
 
 
 OUT_STAMPS = os.path.join(HERE, "libmr_engine_stamps.so")
-OUT_CHECKS = os.path.join(HERE, "libmr_engine_checks.so")
 
 
 def _compile_all(jobs, verbose: bool) -> None:
@@ -60,11 +59,11 @@ def _compile_all(jobs, verbose: bool) -> None:
 
 
 def build(force: bool = False, verbose: bool = False, stamps: bool = True) -> str:
-    """Production library; plus the diagnostic variants (phase timestamps,
-    bounds-checked pull kernels)."""
+    """Production library; plus the diagnostic variant with per-workgroup
+    phase timestamps (libmr_engine_stamps.so)."""
     jobs = [(OUT, [])]
     if stamps:
-        jobs += [(OUT_STAMPS, ["-DMR_STAMPS"]), (OUT_CHECKS, ["-DMR_CHECKS"])]
+        jobs += [(OUT_STAMPS, ["-DMR_STAMPS"])]
     jobs = [(o, x) for o, x in jobs if force or _stale(o)]
     if jobs:
         _compile_all(jobs, verbose)

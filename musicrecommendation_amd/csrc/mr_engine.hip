@@ -40,8 +40,11 @@
 #include <string>
 #include <vector>
 
+#include <atomic>
+
 #include "mr_engine.h"
 #include "mr_internal.h"
+#include "mr_par.h"
 
 
 namespace {
@@ -1778,226 +1781,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// user shape: one 1024-thread workgroup per test user scores the whole shard
-// in one LDS tile, stage 1 included — no neighbour lists in HBM, no tile
-// hand-off, no merge: three dependent gathers (T(u) -> listeners -> their
-// songs) and the top-k, in one launch. For small catalogues (the shard's
-// int64 accumulators + the train users' weights fit the 160 KiB LDS, e.g. the
-// C2 subset: 16770 songs x 500 train users). MR:140-166 / MR:230-257.
-// ---------------------------------------------------------------------------
-constexpr int kUserMaxPerThread = 20;  // songs per thread: 20 x 1024 x 8 B = the whole LDS
-constexpr int kUserPre = 28;           // (train user, song) entries per thread prefetched before stage 1
-// Not chosen automatically: at C2 (10 test users) one workgroup per user
-// leaves 246 CUs idle and serialises a whole row's epilogue and top-k on one
-// CU: 21.2 us vs 14.0 us fused after its stage 2 became LDS-only (31.7 us in
-// round 1; profiles/r02/c2_bs_sweep_user_v2.txt, phase_stamps_c2_user_v2.txt:
-// stage 1 8.4, stage 2 2.6, epilogue 5.6, top-k 4.0 us).
-constexpr bool kUserAuto = false;
-template <int NT>
-struct UserLds {
-  int acc, heard, y, s_scan, wk, ws, fk, fs, gm, total;
-};
-template <int NT>
-__host__ __device__ inline UserLds<NT> user_lds(int bs, int n_tr, int k) {
-  constexpr int NW = NT / 64;
-  const int kk = k > 0 ? k : 1;
-  UserLds<NT> L;
-  int o = 0;
-  const int s1 = NT * 16 + (NT + 1) * 4;  // stage-1 staging (s_lo, s_w, s_pre), aliases acc
-  L.acc = o; o = align16(o + (bs * 8 > s1 ? bs * 8 : s1));
-  L.heard = o; o = align16(o + ((bs + 31) / 32) * 4);
-  L.y = o; o = align16(o + (n_tr > 0 ? n_tr : 1) * 8);
-  L.s_scan = o; o = align16(o + NW * 4);
-  L.wk = o; o = align16(o + NW * kk * 8);
-  L.ws = o; o = align16(o + NW * kk * 4);
-  L.fk = o; o = align16(o + kk * 8);
-  L.fs = o; o = align16(o + kk * 4);
-  L.gm = o; o = align16(o + topk_scratch_bytes<NT>());
-  L.total = o;
-  return L;
-}
-
-template <int MODEL, typename OutT, int KS>
-__global__ __launch_bounds__(kWideThreads) void k_score_user(ScoreParams p) {
-  constexpr int NT = kWideThreads, NW = NT / 64;
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  const UserLds<NT> L = user_lds<NT>(p.block_songs, p.n_tr, p.topk);
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
-  unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
-  unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
-  int* s_scan = reinterpret_cast<int*>(smem_raw + L.s_scan);
-  const int bu = blockIdx.x;
-  const int u = p.user0 + bu;
-  const int tid = threadIdx.x, w = tid >> 6;
-  const int blo = p.song_lo, bhi = p.song_hi, bw = bhi - blo;
-  const double two_f = ldexp(1.0, p.frac_bits);
-  MR_STAMP(0);
-  // this thread's epilogue scales (songs tid + NT j), loaded now: they land
-  // while stages 1-2 run
-  double sc[kUserMaxPerThread];
-#pragma unroll
-  for (int j = 0; j < kUserMaxPerThread; ++j) {
-    const int i = tid + j * NT;
-    sc[j] = (MODEL == MR_IBM && i < bw) ? p.sqrt_c[blo + i] : 1.0;
-  }
-  // stage 2's input, independent of the test user: the shard's (train user,
-  // song) entries (tpack, one contiguous coalesced run), kUserPre per thread
-  const int e1 = p.toff[p.n_tr];
-  unsigned pk[kUserPre];
-#pragma unroll
-  for (int j = 0; j < kUserPre; ++j) {
-    const int i = tid + j * NT;
-    pk[j] = i < e1 ? p.tpack[i] : 0xffffffffu;
-  }
-
-  for (int i = tid; i < p.n_tr; i += NT) Y[i] = 0ull;
-  for (int i = tid; i < (bw + 31) / 32; i += NT) heard[i] = 0u;
-  __syncthreads();
-
-  // stage 1: Y[v] += w(s2) over v in L_tr(s2), s2 in T(u) (MR:140-149 /
-  // MR:230-239), flattened over NT songs of T(u) at a time.
-  {
-    long long* s_lo = reinterpret_cast<long long*>(smem_raw + L.acc);
-    long long* s_w = s_lo + NT;
-    int* s_pre = reinterpret_cast<int*>(s_w + NT);
-    const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
-    for (long long base = t0; base < t1; base += NT) {
-      const int n = (int)min((long long)NT, t1 - base);
-      int len = 0;
-      if (tid < n) {
-        const int s2 = p.te_songs[base + tid];
-        if (p.te_rng) {  // listener range resolved at load time
-          const int2 r = p.te_rng[base + tid];
-          len = r.y;
-          s_lo[tid] = r.x;
-          s_w[tid] = MODEL == MR_IBM ? p.te_q[base + tid] : 1ll;
-        } else {
-          const long long lo = p.trs_off[s2], hi = p.trs_off[s2 + 1];
-          len = (int)(hi - lo);
-          s_lo[tid] = lo;
-          s_w[tid] = MODEL == MR_IBM ? p.q_song[s2] : 1ll;
-        }
-        if (s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
-      }
-      int total;
-      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
-      s_pre[tid] = pre;
-      __syncthreads();
-      constexpr int E = 8;
-      for (int i0 = tid; i0 < total; i0 += E * NT) {
-        int v[E];
-        unsigned long long wv[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int i = i0 + e * NT;
-          v[e] = -1;
-          wv[e] = 0ull;
-          if (i < total) {
-            int a = 0, b = n;  // last song j with s_pre[j] <= i
-            while (b - a > 1) {
-              const int m = (a + b) >> 1;
-              if (s_pre[m] <= i) a = m; else b = m;
-            }
-            v[e] = p.trs_users[s_lo[a] + (i - s_pre[a])];
-            wv[e] = (unsigned long long)s_w[a];
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e)
-          if (v[e] >= 0) atomicAdd(&Y[v[e]], wv[e]);
-      }
-      __syncthreads();
-    }
-  }
-  for (int i = tid; i < bw; i += NT) acc[i] = 0ull;  // the staging above is done
-  __syncthreads();
-  MR_STAMP(1);
-
-  // stage 2: LDS only — every prefetched (train user, song) entry whose user
-  // is a neighbour adds its weight; UBM first turns the overlap counts into
-  // fixed-point cosines in place (MR:142-148).
-  if (MODEL == MR_UBM) {
-    const double rs_u = p.sqrt_te[u];
-    for (int v = tid; v < p.n_tr; v += NT) {
-      const unsigned long long y = Y[v];
-      if (y != 0ull) Y[v] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, p.sqrt_tr[v], two_f);
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int j = 0; j < kUserPre; ++j) {
-    if (pk[j] == 0xffffffffu) continue;
-    const unsigned long long y = Y[pk[j] >> 16];
-    if (y != 0ull) atomicAdd(&acc[pk[j] & 0xffffu], y);
-  }
-  for (int i = tid + kUserPre * NT; i < e1; i += NT) {  // shards of more entries
-    const unsigned e = p.tpack[i];
-    const unsigned long long y = Y[e >> 16];
-    if (y != 0ull) atomicAdd(&acc[e & 0xffffu], y);
-  }
-  __syncthreads();
-  MR_STAMP(2);
-
-  // epilogue: scores -> dense row; keys back into acc (scale loads batched)
-  const double inv_f = ldexp(1.0, -p.frac_bits);
-  OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width;
-  long long mk = kKeyNone;  // this thread's best key (the top-k's first pass)
-  int ms = INT_MAX;
-#pragma unroll
-  for (int j = 0; j < kUserMaxPerThread; ++j) {
-    const int i = tid + j * NT;
-    if (i < bw) {
-      const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
-      double score = (double)(long long)acc[i] * inv_f;
-      if (MODEL == MR_IBM) score = score / sc[j];
-      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
-      const long long key = h ? kKeyNone : __double_as_longlong(score);
-      acc[i] = (unsigned long long)key;
-      if (key >= 0) take_if_before(mk, ms, key, blo + i);
-    }
-  }
-  if (p.topk <= 0) return;
-  const int k = KS == 10 ? 10 : p.topk;
-  __syncthreads();
-  MR_STAMP(3);
-
-  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
-  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
-  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
-  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
-  const bool fast = !p.topk_lists && block_topk_threshold<NT>(
-      bw, k, [&](int i, long long& key, int& song) { key = (long long)acc[i]; song = blo + i; }, mk, ms,
-      smem_raw + L.gm, wk, ws, min(256, NW * k), fk, fs
-#ifdef MR_STAMPS
-      , p.stamps ? p.stamps + (size_t)blockIdx.x * kStampSlots : nullptr
-#endif
-      );
-  if (!fast) {  // many ties at the threshold: per-thread running lists
-    long long tk[KS];
-    int ts[KS];
-#pragma unroll
-    for (int t = 0; t < KS; ++t) { tk[t] = kKeyNone; ts[t] = INT_MAX; }
-    long long thr = kKeyNone;
-    for (int i = tid; i < bw; i += NT) {
-      const long long key = (long long)acc[i];
-      if (key > thr) lane_list_insert(tk, ts, k, key, blo + i, thr);
-    }
-    wave_topk_regs<KS, true>(tk, ts, k, wk + w * k, ws + w * k);
-    __syncthreads();
-    if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
-    __syncthreads();
-  }
-  MR_STAMP(4);
-  for (int r = tid; r < k; r += NT) {
-    const size_t o = (size_t)u * k + r;
-    p.top_key[o] = fk[r];
-    p.top_song[o] = fs[r];
-    p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
-  }
-  MR_STAMP(5);
-}
-
-// ---------------------------------------------------------------------------
 // top-k over a dense model buffer (any model of the context's shape, e.g. a
 // combination model, MR:317-481): one 1024-thread workgroup per test user,
 // per-thread running lists, per-wave register tournament, wave 0 merges.
@@ -2049,200 +1832,10 @@ __global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) 
   }
 }
 
-// ---------------------------------------------------------------------------
-// pull shape (dense neighbourhoods, e.g. 10k x 1k): stage 1 scatters the
-// neighbour weights of a batch of test users into Yt[v][user] (int64 global
-// atomics: exact and order-independent); a pull kernel then gives each wave
-// 64 users (lanes) and walks songs: acc[u] = Σ_{v ∈ L_tr(s)} Yt[v][u] is a
-// 512-byte coalesced row gather per listener, summed in registers (no
-// atomics, no tiles of accumulators). Scores go through a per-wave LDS tile
-// for row-contiguous stores; each lane keeps a running top-k of its user.
-// ---------------------------------------------------------------------------
-
-// Bounds-checked diagnostic build (-DMR_CHECKS, libmr_engine_checks.so): an
-// out-of-range index is recorded in *dbg (bit = code) and replaced by 0.
-#ifdef MR_CHECKS
-#define MR_IDX(i, n, code) \
-  (((unsigned long long)(i) < (unsigned long long)(n)) ? (i) : (atomicOr(p.dbg, (code)), (decltype(i))0))
-#else
-#define MR_IDX(i, n, code) (i)
-#endif
-
-constexpr int kPullLanes = 64;   // users per wave
-constexpr int kPullChunk = 32;   // songs per staged output tile
-constexpr int kPullMaxK = 16;    // running top-k slots per lane (registers)
 // auto shape: wide from this many (test user x train user) pairs of work
 // (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt: wide wins
 // from 500 x 256 and 2000 x 100, fused below 500 x 128 and 2000 x 32)
 constexpr long long kWideMinUserPairs = 100000;
-
-struct ColParams {
-  int n_tr, user0, te_stride, frac_bits;
-  const long long* te_off;
-  const int* te_songs;
-  const long long* trs_off;
-  const int* trs_users;
-  const long long* q_song;
-  const double* sqrt_tr;
-  const double* sqrt_te;
-  unsigned long long* Yt;    // [n_tr][te_stride]: column bu = batch user bu
-  unsigned* dbg;             // MR_CHECKS builds
-  long long n_yt;
-};
-
-// Stage 1 of the pull shape: one workgroup per test user accumulates Y[v] in
-// LDS (as k_neighbours) and stores the whole column Yt[.][bu], zeros
-// included, so Yt needs no clearing between runs. UBM weights are final
-// fixed-point cosines here (MR:142-148).
-template <int MODEL>
-__global__ __launch_bounds__(kThreads) void k_stage1_columns(ColParams p) {
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw);         // [n_tr]
-  long long* s_lo = reinterpret_cast<long long*>(smem_raw + align16(p.n_tr * 8));  // [256]
-  long long* s_w = s_lo + kThreads;                                                // [256]
-  int* s_pre = reinterpret_cast<int*>(s_w + kThreads);                             // [257]
-  int* s_scan = s_pre + kThreads + 4;                                              // [kWaves]
-  const int bu = blockIdx.x;
-  const int u = p.user0 + bu;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
-  __syncthreads();
-  accumulate_neighbours<MODEL>(Y, p.te_off[u], p.te_off[u + 1], p.te_songs, p.trs_off, p.trs_users, p.q_song,
-                               s_lo, s_w, s_pre, s_scan, nullptr, 0, 0);
-  const double two_f = ldexp(1.0, p.frac_bits);
-  const double rs_u = p.sqrt_te[u];
-  unsigned long long* col = p.Yt + bu;
-  for (int v = tid; v < p.n_tr; v += kThreads) {
-    const unsigned long long y = Y[v];
-    col[MR_IDX((size_t)v * p.te_stride + bu, (size_t)p.n_yt, 1u) - bu] =
-        y ? (unsigned long long)neighbour_weight<MODEL>(y, rs_u, MODEL == MR_UBM ? p.sqrt_tr[v] : 0.0, two_f) : 0ull;
-  }
-}
-
-struct PullParams {
-  int user0, n_users, te_stride;
-  int song_lo, song_hi, width, range, n_ranges;
-  int frac_bits, topk, dense;
-  const unsigned long long* Yt;
-  const long long* trs_off;
-  const int* trs_users;
-  const double* sqrt_c;
-  const long long* te_off;       // heard songs: the sorted T(u), walked per lane
-  const int* te_songs;
-  void* dense_out;               // [n_te][width]
-  long long* cand_key;           // [te_stride][n_ranges][k] (batch-local users)
-  int* cand_song;
-  unsigned* dbg;                 // MR_CHECKS builds: sizes of the arrays above
-  long long n_yt, n_trs, n_te_songs, n_te_off, n_songs1, n_dense, n_cand;
-};
-
-template <int MODEL, typename OutT>
-__global__ __launch_bounds__(kThreads) void k_pull(PullParams p) {
-  __shared__ OutT tile[kWaves][kPullLanes][kPullChunk + 1];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int range = blockIdx.x;
-  const int bu0 = (blockIdx.y * kWaves + w) * kPullLanes;  // this wave's first batch user
-  if (bu0 >= p.n_users) return;                              // whole wave idle (wave-uniform)
-  const int bu = bu0 + lane;
-  const bool uok = bu < p.n_users;
-  const int s_begin = p.song_lo + range * p.range;
-  const int s_end = min(p.song_hi, s_begin + p.range);
-  const double inv_f = ldexp(1.0, -p.frac_bits);
-  const unsigned long long* yrow = p.Yt + bu0 + lane;       // + v * te_stride
-  // next heard song of this lane's user at or after s_begin (songs ascend)
-  long long hp = 0, hend = 0;
-  if (uok) {
-    long long a = p.te_off[MR_IDX(p.user0 + bu, p.n_te_off, 2u)], b = p.te_off[MR_IDX(p.user0 + bu + 1, p.n_te_off, 2u)];
-    hend = b;
-    while (a < b) {
-      const long long m = (a + b) >> 1;
-      if (p.te_songs[MR_IDX(m, p.n_te_songs, 4u)] < s_begin) a = m + 1; else b = m;
-    }
-    hp = a;
-  }
-  int next_heard = hp < hend ? p.te_songs[MR_IDX(hp, p.n_te_songs, 4u)] : INT_MAX;
-  OutT (*tw)[kPullChunk + 1] = tile[w];
-  const int k = p.topk;
-  long long tk[kPullMaxK];
-  int ts[kPullMaxK];
-#pragma unroll
-  for (int j = 0; j < kPullMaxK; ++j) { tk[j] = kKeyNone; ts[j] = INT_MAX; }
-  long long thr = kKeyNone;  // current k-th key of this lane's list
-
-  for (int c0 = s_begin; c0 < s_end; c0 += kPullChunk) {
-    const int cn = min(kPullChunk, s_end - c0);
-    for (int j = 0; j < cn; ++j) {
-      const int s = c0 + j;
-      const long long x0 = p.trs_off[MR_IDX(s, p.n_songs1, 8u)], x1 = p.trs_off[MR_IDX(s + 1, p.n_songs1, 8u)];
-      unsigned long long acc = 0ull;
-      long long x = x0;
-      for (; x + 4 <= x1; x += 4) {  // 4 row gathers in flight
-        const int v0 = p.trs_users[MR_IDX(x, p.n_trs, 16u)], v1 = p.trs_users[MR_IDX(x + 1, p.n_trs, 16u)];
-        const int v2 = p.trs_users[MR_IDX(x + 2, p.n_trs, 16u)], v3 = p.trs_users[MR_IDX(x + 3, p.n_trs, 16u)];
-        const size_t yo = bu0 + lane;
-        const unsigned long long a0 = yrow[MR_IDX((size_t)v0 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
-        const unsigned long long a1 = yrow[MR_IDX((size_t)v1 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
-        const unsigned long long a2 = yrow[MR_IDX((size_t)v2 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
-        const unsigned long long a3 = yrow[MR_IDX((size_t)v3 * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
-        acc += (a0 + a1) + (a2 + a3);
-      }
-      for (; x < x1; ++x) {
-        const size_t yo = bu0 + lane;
-        const int v = p.trs_users[MR_IDX(x, p.n_trs, 16u)];
-        acc += yrow[MR_IDX((size_t)v * p.te_stride + yo, (size_t)p.n_yt, 32u) - yo];
-      }
-      double score = (double)(long long)acc * inv_f;
-      if (MODEL == MR_IBM) score = score / p.sqrt_c[s];
-      const bool h = s == next_heard;
-      if (h) {
-        ++hp;
-        next_heard = hp < hend ? p.te_songs[MR_IDX(hp, p.n_te_songs, 4u)] : INT_MAX;
-      }
-      tw[lane][j] = h ? (OutT)NAN : (OutT)score;
-      // running top-k: songs arrive in increasing order, so an equal key never
-      // displaces an earlier (lower-id) song
-      const long long key = h ? kKeyNone : __double_as_longlong(score);
-      if (k > 0 && key > thr) {
-        long long ck = key;
-        int cs = s;
-#pragma unroll
-        for (int t = 0; t < kPullMaxK; ++t) {
-          const bool b = t < k && cand_before(ck, cs, tk[t], ts[t]);
-          const long long ok = tk[t];
-          const int os = ts[t];
-          tk[t] = b ? ck : tk[t];
-          ts[t] = b ? cs : ts[t];
-          ck = b ? ok : ck;
-          cs = b ? os : cs;
-        }
-        long long nt = kKeyNone;
-#pragma unroll
-        for (int t = 0; t < kPullMaxK; ++t) nt = (t == k - 1) ? tk[t] : nt;
-        thr = nt;
-      }
-    }
-    if (p.dense) {  // flush the wave's [64 users][cn songs] tile, two rows per store
-      wave_lds_sync();
-      OutT* out = reinterpret_cast<OutT*>(p.dense_out);
-      const int r_half = lane >> 5, col = lane & 31;
-      for (int r0 = 0; r0 < kPullLanes; r0 += 2) {
-        const int r = r0 + r_half;
-        if (bu0 + r < p.n_users && col < cn)
-          out[MR_IDX((size_t)(p.user0 + bu0 + r) * p.width + (c0 - p.song_lo) + col, (size_t)p.n_dense, 64u)] =
-              tw[r][col];
-      }
-      wave_lds_sync();
-    }
-  }
-  if (k > 0 && uok) {
-    const size_t co = MR_IDX(((size_t)bu * p.n_ranges + range) * k + (k - 1), (size_t)p.n_cand, 128u) - (k - 1);
-    long long* ck = p.cand_key + co;
-    int* cs = p.cand_song + co;
-#pragma unroll
-    for (int t = 0; t < kPullMaxK; ++t)
-      if (t < k) { ck[t] = tk[t]; cs[t] = tk[t] >= 0 ? ts[t] : -1; }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Top-k merge over lists (exchange step after a song-shard all-gather).
@@ -2256,8 +1849,6 @@ struct MergeParams {
   long long* out_keys;    // [n_users][k_out]
   int* out_songs;
   double* out_scores;     // may be null
-  unsigned* dbg;          // MR_CHECKS builds (0 sizes = unchecked)
-  long long n_in, n_out;
 };
 
 __host__ __device__ inline int merge_lds_bytes(int k) {
@@ -2282,10 +1873,7 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
     for (int i = tid; i < nl * k; i += kThreads) {
       const int l = done + i / k, r = i - (i / k) * k;
       const bool in = r < p.k_in;
-      size_t src = (size_t)l * p.list_stride + r;
-#ifdef MR_CHECKS
-      if (p.n_in && in) src = MR_IDX(src + (size_t)bu * p.user_stride, (size_t)p.n_in, 256u) - (size_t)bu * p.user_stride;
-#endif
+      const size_t src = (size_t)l * p.list_stride + r;
       mk[off * k + i] = in ? keys[src] : kKeyNone;
       ms[off * k + i] = in ? songs[src] : -1;
     }
@@ -2299,14 +1887,32 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
     done += nl;
     off = 1;
   }
-  size_t o = (size_t)bu * k;
-#ifdef MR_CHECKS
-  if (p.n_out) o = MR_IDX(o + k - 1, (size_t)p.n_out, 512u) - (k - 1);
-#endif
+  const size_t o = (size_t)bu * k;
   for (int r = tid; r < k; r += kThreads) {
     p.out_keys[o + r] = fk[r];
     p.out_songs[o + r] = fs[r];
     if (p.out_scores) p.out_scores[o + r] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stage-1 chunk boundaries of every listener list, built once by mr_load:
+// sbound[s][cc] = first index i of L_tr(s) = trs_users[trs_off[s] ..
+// trs_off[s+1]) (ascending) with trs_users[i] >= cc * chunk. One binary search
+// per entry (C4: 95M entries; was a host loop plus a 380 MB upload).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sbound(const long long* trs_off, const int* trs_users, int n_s, int nc1,
+                                                int chunk, int* sbound) {
+  const size_t total = (size_t)n_s * nc1;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int s = (int)(i / nc1);
+    const long long bound = (long long)(int)(i - (size_t)s * nc1) * chunk;
+    long long a = trs_off[s], b = trs_off[s + 1];
+    while (a < b) {
+      const long long m = (a + b) >> 1;
+      if (trs_users[m] < bound) a = m + 1; else b = m;
+    }
+    sbound[i] = (int)a;
   }
 }
 
@@ -2343,11 +1949,9 @@ int dev_upload(DevBuf<T>& b, const T* src, size_t n, hipStream_t st) {
 
 using ScoreKernel = void (*)(ScoreParams);
 using NbrKernel = void (*)(NbrParams);
-using ColKernel = void (*)(ColParams);
-using PullKernel = void (*)(PullParams);
 
 // Launch shapes (mr_options.stage1 / mr_launch_info).
-enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapePull = 2, kShapeWide = 3, kShapeUser = 4 };
+enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapeWide = 3 };
 
 }  // namespace
 
@@ -2358,7 +1962,6 @@ struct mr_ctx {
   bool ran = false;
   bool fused = false;
   int shape = kShapeSeparate;
-  int te_stride = 0;  // pull: Yt row length (batch padded to 64 users)
   int last_model = -1;
   int n_tr = 0, n_te = 0, n_s = 0;
   int song_lo = 0, song_hi = 0, width = 0;
@@ -2368,10 +1971,6 @@ struct mr_ctx {
   size_t score_lds = 0, nbr_lds = 0, merge_lds = 0, wide_lds = 0;
   ScoreKernel score_kernel[2] = {nullptr, nullptr};  // [model]
   NbrKernel nbr_kernel[2] = {nullptr, nullptr};
-  ColKernel col_kernel[2] = {nullptr, nullptr};
-  PullKernel pull_kernel[2] = {nullptr, nullptr};
-  DevBuf<unsigned long long> yt;
-  DevBuf<unsigned> dbg;  // MR_CHECKS builds: out-of-range index bits
   DevBuf<long long> tr_off, te_off, trs_off, q_song, cand_key, top_key, nbr_q;
   DevBuf<int> te_songs, trs_users, toff, nbr_v, nbr_cnt, cand_song, top_song;
   DevBuf<unsigned short> tsongs;
@@ -2412,8 +2011,6 @@ struct mr_ctx {
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
     dense.release();
     stamps.release();
-    yt.release();
-    dbg.release();
     flag.release();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -2426,11 +2023,38 @@ struct mr_ctx {
 
 namespace {
 
+// Smallest i in [0, n) with bad(i), or -1: every worker scans its range in
+// order and stops at its first hit.
+template <class F>
+int64_t first_bad(int64_t n, F&& bad, int64_t grain = 1 << 14) {
+  std::atomic<int64_t> best{INT64_MAX};
+  mr_par::parallel_for(n, [&](int64_t lo, int64_t hi, int) {
+    for (int64_t i = lo; i < hi && i < best.load(std::memory_order_relaxed); ++i)
+      if (bad(i)) {
+        int64_t cur = best.load();
+        while (i < cur && !best.compare_exchange_weak(cur, i)) {}
+        return;
+      }
+  }, grain);
+  const int64_t b = best.load();
+  return b == INT64_MAX ? -1 : b;
+}
+
+// Sorted strictly ascending columns in [0, n_cols), checked in parallel; the
+// first bad row (in row order) is reported. Offsets are checked first, so the
+// column pass only reads inside [off[0], off[n_rows]).
 int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, const int32_t* col) {
   if (!off || (off[n_rows] > 0 && !col)) return fail(MR_E_INVALID, "%s: null CSR array", what);
   if (off[0] != 0) return fail(MR_E_INVALID, "%s: offsets[0] = %lld != 0", what, (long long)off[0]);
-  for (int r = 0; r < n_rows; ++r) {
-    if (off[r + 1] < off[r]) return fail(MR_E_INVALID, "%s: offsets decrease at row %d", what, r);
+  const int64_t r0 = first_bad(n_rows, [&](int64_t r) { return off[r + 1] < off[r]; });
+  if (r0 >= 0) return fail(MR_E_INVALID, "%s: offsets decrease at row %d", what, (int)r0);
+  const int64_t r1 = first_bad(n_rows, [&](int64_t r) {
+    for (int64_t i = off[r]; i < off[r + 1]; ++i)
+      if (col[i] < 0 || col[i] >= n_cols || (i > off[r] && col[i] <= col[i - 1])) return true;
+    return false;
+  }, 1 << 10);
+  if (r1 >= 0) {
+    const int r = (int)r1;
     for (int64_t i = off[r]; i < off[r + 1]; ++i) {
       if (col[i] < 0 || col[i] >= n_cols)
         return fail(MR_E_INVALID, "%s: row %d has column %d outside [0,%d)", what, r, col[i], n_cols);
@@ -2441,6 +2065,20 @@ int validate_csr(const char* what, int n_rows, int n_cols, const int64_t* off, c
   if (off[n_rows] >= (int64_t)INT32_MAX)
     return fail(MR_E_INVALID, "%s: %lld entries exceed the int32 index range", what, (long long)off[n_rows]);
   return MR_OK;
+}
+
+// Worker ranges over [0, n) with about equal weight: range w = [cut[w], cut[w+1])
+// of a prefix-summed weight (CSR offsets: rows of power-law length).
+std::vector<int64_t> weighted_cuts(const int64_t* prefix, int64_t n, int parts) {
+  std::vector<int64_t> cut(parts + 1, n);
+  cut[0] = 0;
+  const int64_t total = prefix[n] - prefix[0];
+  for (int w = 1; w < parts; ++w) {
+    const int64_t target = prefix[0] + total * w / parts;
+    cut[w] = std::max(cut[w - 1], (int64_t)(std::lower_bound(prefix, prefix + n + 1, target) - prefix));
+    cut[w] = std::min(cut[w], n);
+  }
+  return cut;
 }
 
 // Rows of the in-launch merge's threshold pass: 32 (C2 step 20.4 us vs 22.9 at
@@ -2493,13 +2131,6 @@ void pick_kernels(mr_ctx* c) {
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, true> : k_score<MODEL, float, true>;
   else
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
-  if (c->shape == kShapeUser) {
-    if (c->opt.topk == 10)
-      c->score_kernel[MODEL] = f64 ? k_score_user<MODEL, double, 10> : k_score_user<MODEL, float, 10>;
-    else
-      c->score_kernel[MODEL] = f64 ? k_score_user<MODEL, double, kMaxTopkLarge>
-                                   : k_score_user<MODEL, float, kMaxTopkLarge>;
-  }
   if (c->shape == kShapeWide) {
     if (c->opt.topk == 10)
       c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, 10>
@@ -2509,33 +2140,21 @@ void pick_kernels(mr_ctx* c) {
                                    : k_score_wide<MODEL, float, kWideThreads, kMaxTopkLarge>;
   }
   c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
-  c->col_kernel[MODEL] = k_stage1_columns<MODEL>;
-  c->pull_kernel[MODEL] = f64 ? k_pull<MODEL, double> : k_pull<MODEL, float>;
-}
-
-// Pull shape: songs per range so that the grid has >= ~2048 workgroups
-// (4 x 64 users each), a multiple of kPullChunk.
-int pull_range(int width, int batch) {
-  const long long wy = (batch + kWaves * kPullLanes - 1) / (kWaves * kPullLanes);
-  long long r = ((long long)width * wy + 2047) / 2048;
-  r = (r + kPullChunk - 1) / kPullChunk * kPullChunk;
-  return (int)std::max<long long>(64, std::min<long long>(r, 8192));
 }
 
 // Launch-shape rule of mr_load (also answers mr_shard_tile_songs before any
-// load). auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt):
-// wide beats separate and pull above 4096 train users, and fused from ~1e5
-// (test user x train user) pairs; fused for small sets (C2).
-int pick_shape(const mr_options& o, int n_tr, int n_te, bool user_fits) {
+// load). auto (scripts/shape_sweep.py, profiles/r01_final/shape_sweep.txt):
+// wide beats separate above 4096 train users, and fused from ~1e5 (test user x
+// train user) pairs; fused for small sets (C2). Round 2 also measured a
+// "pull" shape (dense Yt slab gathered per song) and a "user" shape (one
+// 1024-thread workgroup per test user): never faster, removed in round 3.
+int pick_shape(const mr_options& o, int n_tr, int n_te) {
   const int k = o.topk;
   if (o.stage1 == 1) return kShapeFused;
   if (o.stage1 == 2) return kShapeSeparate;
-  if (o.stage1 == 3) return kShapePull;
   if (o.stage1 == 4) return kShapeWide;
-  if (o.stage1 == 5) return kShapeUser;
   if (n_tr > kMaxFusedTrainUsers && k <= kMaxTopkLarge) return kShapeWide;
   if ((long long)n_te * n_tr >= kWideMinUserPairs && k <= kMaxTopkLarge) return kShapeWide;
-  if (user_fits && kUserAuto) return kShapeUser;
   return n_tr <= kMaxFusedTrainUsers ? kShapeFused : kShapeSeparate;
 }
 
@@ -2587,10 +2206,9 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
       (o.block_songs % 256) != 0)
     return fail(MR_E_INVALID, "block_songs %d must be a multiple of 256 in [0,%d]", o.block_songs,
                 o.stage1 == 4 ? kMaxWideBlockSongs : kMaxBlockSongs);
-  if (o.stage1 < 0 || o.stage1 > 5) return fail(MR_E_INVALID, "stage1 %d outside [0,5]", o.stage1);
+  if (o.stage1 < 0 || o.stage1 > 4 || o.stage1 == 3)
+    return fail(MR_E_INVALID, "stage1 %d is not 0 (auto), 1 (fused), 2 (separate) or 4 (wide)", o.stage1);
   if (o.topk_lists != 0 && o.topk_lists != 1) return fail(MR_E_INVALID, "topk_lists %d not 0 or 1", o.topk_lists);
-  if (o.stage1 == 5 && o.block_songs != 0)
-    return fail(MR_E_INVALID, "user shape scores the whole shard in one tile: block_songs must be 0");
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
@@ -2644,6 +2262,7 @@ void* mr_stream(const mr_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (!c || !d) return fail(MR_E_INVALID, "null argument");
+  mr_par::PhaseTrace trace("MR_LOAD_TRACE", "mr_load");
   MR_HIP(hipSetDevice(c->opt.device));
   MR_HIP(hipStreamSynchronize(c->stream));
   c->ring_used = 0;
@@ -2658,118 +2277,151 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = validate_csr("train user->songs", n_tr, n_s, d->tr_off, d->tr_songs))) return rc;
   if ((rc = validate_csr("test user->songs", n_te, n_s, d->te_off, d->te_songs))) return rc;
   if (!d->song_count || !d->tr_len || !d->te_len) return fail(MR_E_INVALID, "null count arrays");
-  // Transpose: song -> train users (sorted, since v ascends) and count checks.
-  std::vector<int64_t> trs_off(n_s + 1, 0);
+  {  // lengths count duplicates: >= the distinct count, and nobody is empty (MR:44-46)
+    const int64_t v = first_bad(n_tr, [&](int64_t v) {
+      const int64_t deg = d->tr_off[v + 1] - d->tr_off[v];
+      return deg <= 0 || d->tr_len[v] < deg;
+    });
+    if (v >= 0)
+      return fail(MR_E_INVALID, "train user %d: %lld distinct songs but length %d", (int)v,
+                  (long long)(d->tr_off[v + 1] - d->tr_off[v]), d->tr_len[v]);
+    const int64_t u = first_bad(n_te, [&](int64_t u) {
+      const int64_t deg = d->te_off[u + 1] - d->te_off[u];
+      return deg <= 0 || d->te_len[u] < deg;
+    });
+    if (u >= 0)
+      return fail(MR_E_INVALID, "test user %d: %lld distinct songs but length %d", (int)u,
+                  (long long)(d->te_off[u + 1] - d->te_off[u]), d->te_len[u]);
+  }
+  trace("validate");
+  const int64_t nnz_tr = d->tr_off[n_tr];
+  // Workers of the bulk passes: ranges of users with about equal entries.
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(mr_par::usable_cores(), nnz_tr >> 18));
+  // Distinct listeners per song: train (per-worker histograms) and test.
   std::vector<int32_t> col_tr(n_s, 0), col_te(n_s, 0);
-  for (int v = 0; v < n_tr; ++v) {
-    const int64_t deg = d->tr_off[v + 1] - d->tr_off[v];
-    if (deg <= 0 || d->tr_len[v] < deg)
-      return fail(MR_E_INVALID, "train user %d: %lld distinct songs but length %d", v, (long long)deg, d->tr_len[v]);
-    for (int64_t i = d->tr_off[v]; i < d->tr_off[v + 1]; ++i) col_tr[d->tr_songs[i]]++;
+  {
+    std::vector<std::vector<int32_t>> h(W);
+    const std::vector<int64_t> cut = weighted_cuts(d->tr_off, n_tr, W);
+    mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+      for (int64_t w = w0; w < w1; ++w) {
+        h[w].assign(n_s, 0);
+        for (int64_t i = d->tr_off[cut[w]]; i < d->tr_off[cut[w + 1]]; ++i) h[w][d->tr_songs[i]]++;
+      }
+    }, 1, W);
+    mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
+      for (int w = 0; w < W; ++w)
+        for (int64_t s2 = a; s2 < b; ++s2) col_tr[s2] += h[w][s2];
+    }, 4096);
   }
-  for (int u = 0; u < n_te; ++u) {
-    const int64_t deg = d->te_off[u + 1] - d->te_off[u];
-    if (deg <= 0 || d->te_len[u] < deg)
-      return fail(MR_E_INVALID, "test user %d: %lld distinct songs but length %d", u, (long long)deg, d->te_len[u]);
-    for (int64_t i = d->te_off[u]; i < d->te_off[u + 1]; ++i) col_te[d->te_songs[i]]++;
+  for (int64_t i = 0; i < d->te_off[n_te]; ++i) col_te[d->te_songs[i]]++;
+  {
+    const int64_t s_bad = first_bad(n_s, [&](int64_t s2) {
+      return d->song_count[s2] < col_tr[s2] + col_te[s2] || d->song_count[s2] <= 0;
+    });
+    if (s_bad >= 0)
+      return fail(MR_E_INVALID, "song %d: count %d below its %d distinct listeners (or zero)", (int)s_bad,
+                  d->song_count[s_bad], col_tr[s_bad] + col_te[s_bad]);
   }
-  for (int s = 0; s < n_s; ++s) {
-    if (d->song_count[s] < col_tr[s] + col_te[s] || d->song_count[s] <= 0)
-      return fail(MR_E_INVALID, "song %d: count %d below its %d distinct listeners (or zero)", s,
-                  d->song_count[s], col_tr[s] + col_te[s]);
-    trs_off[s + 1] = trs_off[s] + col_tr[s];
-  }
+  std::vector<int64_t> trs_off((size_t)n_s + 1, 0);
+  for (int s2 = 0; s2 < n_s; ++s2) trs_off[s2 + 1] = trs_off[s2] + col_tr[s2];
+  trace("counts");
   // Train users renumbered by distinct-song count, descending (ties by id),
   // unless opt.train_order = 1: the users of one wave then have segments of
   // similar length in every song tile, so no lane waits on one heavy
   // listener's long tail (heavy listeners dominate every neighbourhood).
   // Results do not change: every accumulation is an order-free integer sum
-  // and the outputs are indexed by test user and song only.
+  // and the outputs are indexed by test user and song only. (A stable
+  // counting sort by degree.)
   std::vector<int32_t> perm(std::max(1, n_tr));  // new id -> caller's id
-  for (int v = 0; v < n_tr; ++v) perm[v] = v;
-  if (c->opt.train_order == 0)
-    std::stable_sort(perm.begin(), perm.begin() + n_tr, [&](int a, int b) {
-      return d->tr_off[a + 1] - d->tr_off[a] > d->tr_off[b + 1] - d->tr_off[b];
-    });
-  std::vector<int64_t> p_off((size_t)n_tr + 1, 0);
-  std::vector<int32_t> p_songs(std::max<int64_t>(1, d->tr_off[n_tr])), p_len(std::max(1, n_tr));
-  for (int v = 0; v < n_tr; ++v) {
-    const int o = perm[v];
-    const int64_t a = d->tr_off[o], b = d->tr_off[o + 1];
-    std::copy(d->tr_songs + a, d->tr_songs + b, p_songs.begin() + p_off[v]);
-    p_off[v + 1] = p_off[v] + (b - a);
-    p_len[v] = d->tr_len[o];
+  if (c->opt.train_order == 0 && n_tr > 0) {
+    int64_t max_deg = 0;
+    for (int v = 0; v < n_tr; ++v) max_deg = std::max(max_deg, d->tr_off[v + 1] - d->tr_off[v]);
+    std::vector<int64_t> at((size_t)max_deg + 1, 0);
+    for (int v = 0; v < n_tr; ++v) at[max_deg - (d->tr_off[v + 1] - d->tr_off[v])]++;
+    int64_t run = 0;
+    for (auto& x : at) { const int64_t n = x; x = run; run += n; }
+    for (int v = 0; v < n_tr; ++v) perm[at[max_deg - (d->tr_off[v + 1] - d->tr_off[v])]++] = v;
+  } else {
+    for (int v = 0; v < n_tr; ++v) perm[v] = v;
   }
+  std::vector<int64_t> p_off((size_t)n_tr + 1, 0);
+  mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
+    for (int64_t v = a; v < b; ++v) p_off[v] = d->tr_off[perm[v] + 1] - d->tr_off[perm[v]];
+  });
+  p_off[n_tr] = mr_par::exclusive_scan(p_off.data(), (int64_t)n_tr);
+  mr_par::buffer<int32_t> p_songs((size_t)std::max<int64_t>(1, nnz_tr));
+  std::vector<int32_t> p_len(std::max(1, n_tr));
+  mr_par::parallel_dynamic(n_tr, 2048, [&](int64_t v, int) {
+    const int o = perm[v];
+    std::copy(d->tr_songs + d->tr_off[o], d->tr_songs + d->tr_off[o + 1], p_songs.begin() + p_off[v]);
+    p_len[v] = d->tr_len[o];
+  });
   const int64_t* tr_off = p_off.data();
   const int32_t* tr_songs = p_songs.data();
   const int32_t* tr_len = p_len.data();
-  std::vector<int32_t> trs_users(std::max<int64_t>(1, trs_off[n_s]));
+  trace("renumber");
+  // Transpose song -> train users, lists ascending in v: worker w owns a
+  // contiguous range of (new) users and a private cursor per song.
+  const std::vector<int64_t> ucut = weighted_cuts(tr_off, n_tr, W);
+  mr_par::buffer<int32_t> trs_users((size_t)std::max<int64_t>(1, trs_off[n_s]));
   {
-    std::vector<int64_t> fill(trs_off.begin(), trs_off.end() - 1);
-    for (int v = 0; v < n_tr; ++v)
-      for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) trs_users[fill[tr_songs[i]]++] = v;
+    std::vector<std::vector<int64_t>> pos(W);
+    mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+      for (int64_t w = w0; w < w1; ++w) {
+        pos[w].assign(n_s, 0);
+        for (int64_t i = tr_off[ucut[w]]; i < tr_off[ucut[w + 1]]; ++i) pos[w][tr_songs[i]]++;
+      }
+    }, 1, W);
+    mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
+      for (int64_t s2 = a; s2 < b; ++s2) {
+        int64_t at = trs_off[s2];
+        for (int w = 0; w < W; ++w) {
+          const int64_t n = pos[w][s2];
+          pos[w][s2] = at;
+          at += n;
+        }
+      }
+    }, 4096);
+    mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+      for (int64_t w = w0; w < w1; ++w)
+        for (int64_t v = ucut[w]; v < ucut[w + 1]; ++v)
+          for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) trs_users[pos[w][tr_songs[i]]++] = (int32_t)v;
+    }, 1, W);
   }
+  trace("transpose");
   // Shard geometry and launch shape.
   const int lo = c->opt.song_lo, hi = c->opt.song_hi > 0 ? c->opt.song_hi : n_s;
   if (lo < 0 || hi > n_s || lo >= hi) return fail(MR_E_INVALID, "song shard [%d,%d) invalid for %d songs", lo, hi, n_s);
   const int width = hi - lo;
-  // Shape: many test users -> pull (dense Yt, gathers by song); few users and
-  // a small train set -> fused; otherwise separate.
   const int k = c->opt.topk;
-  const bool user_fits = k <= kMaxTopkLarge && n_tr <= kMaxFusedTrainUsers && width <= kMaxWideBlockSongs &&
-                         user_lds<kWideThreads>((width + 255) / 256 * 256, n_tr, k).total <= kLdsBytes;
-  const int shape = pick_shape(c->opt, n_tr, n_te, user_fits);
-  const bool fused = shape == kShapeFused, pull = shape == kShapePull, wide = shape == kShapeWide,
-             user = shape == kShapeUser;
-  const int user_bs = (width + 255) / 256 * 256;
-  if (user) {
-    if (k > kMaxTopkLarge) return fail(MR_E_INVALID, "user shape keeps topk <= %d (got %d)", kMaxTopkLarge, k);
-    if (user_bs > kMaxWideBlockSongs || user_bs > kUserMaxPerThread * kWideThreads ||
-        user_lds<kWideThreads>(user_bs, n_tr, k).total > kLdsBytes)
-      return fail(MR_E_INVALID, "user shape: %d songs x %d train users need more than %d B of LDS", width, n_tr,
-                  kLdsBytes);
-  }
+  const int shape = pick_shape(c->opt, n_tr, n_te);
+  const bool fused = shape == kShapeFused, wide = shape == kShapeWide;
   if (wide && k > kMaxTopkLarge)
     return fail(MR_E_INVALID, "wide shape keeps topk <= %d (got %d)", kMaxTopkLarge, k);
   if (fused && n_tr > kMaxFusedTrainUsers)
     return fail(MR_E_INVALID, "fused stage 1 needs n_train_users <= %d (got %d)", kMaxFusedTrainUsers, n_tr);
-  if (pull && k > kPullMaxK) return fail(MR_E_INVALID, "pull shape keeps topk <= %d (got %d)", kPullMaxK, k);
-  if (pull && n_tr > kMaxLdsTrainUsers)
-    return fail(MR_E_INVALID, "pull shape needs n_train_users <= %d (got %d)", kMaxLdsTrainUsers, n_tr);
-  // Stage 1 of the separate shape: one LDS chunk of train users per workgroup.
+  // Stage 1 of the separate / wide shapes: one LDS chunk of train users per workgroup.
   const int chunk = stage1_chunk_for(c->opt, n_tr);
   if ((n_tr + chunk - 1) / chunk > kMaxChunks)
     return fail(MR_E_INVALID, "stage1_chunk %d gives more than %d chunks", chunk, kMaxChunks);
   const int n_chunks = (std::max(1, n_tr) + chunk - 1) / chunk;
-  // Pull: test-user batches so that Yt (n_tr x batch int64) fits 16 GiB.
-  const size_t yt_budget = (size_t)16 << 30;
-  const int pull_batch =
-      (int)std::max<size_t>(kPullLanes, std::min<size_t>((size_t)(n_te + kPullLanes - 1) / kPullLanes * kPullLanes,
-                                                         yt_budget / ((size_t)std::max(1, n_tr) * 8) / kPullLanes *
-                                                             kPullLanes));
   int bs;
-  if (pull) {
-    bs = c->opt.block_songs > 0 ? c->opt.block_songs : pull_range(width, std::min(n_te, pull_batch));
-  } else if (user) {
-    bs = user_bs;  // one tile: the whole shard
+  if (wide) {
+    // the widest tile the LDS holds (every tile re-walks the user's whole
+    // neighbour list), then balanced: n_tiles = ceil(width / max), bs =
+    // ceil(width / n_tiles) rounded up to 256
+    const int bmax = wide_bmax(k, n_chunks);
+    const long long nt = ((long long)width + bmax - 1) / bmax;
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs
+                                : (int)std::min<long long>(bmax, (((long long)width + nt - 1) / nt + 255) / 256 * 256);
+    if (wide_lds<kWideThreads>(bs, k, n_chunks).total > kLdsBytes)
+      return fail(MR_E_INVALID, "wide shape: block_songs %d needs more than %d B of LDS", bs, kLdsBytes);
   } else {
-    if (wide) {
-      // the widest tile the LDS holds (every tile re-walks the user's whole
-      // neighbour list), then balanced: n_tiles = ceil(width / max), bs =
-      // ceil(width / n_tiles) rounded up to 256
-      const int bmax = wide_bmax(k, n_chunks);
-      const long long nt = ((long long)width + bmax - 1) / bmax;
-      bs = c->opt.block_songs > 0 ? c->opt.block_songs
-                                  : (int)std::min<long long>(bmax, (((long long)width + nt - 1) / nt + 255) / 256 * 256);
-      if (wide_lds<kWideThreads>(bs, k, n_chunks).total > kLdsBytes)
-        return fail(MR_E_INVALID, "wide shape: block_songs %d needs more than %d B of LDS", bs, kLdsBytes);
-    } else {
-      bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k, n_tr);
-    }
-    if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
-    if (k > kMaxTopkLarge && bs > kMaxTopkTile)
-      return fail(MR_E_INVALID, "with topk > %d block_songs must be <= %d (got %d)", kMaxTopkLarge, kMaxTopkTile, bs);
+    bs = c->opt.block_songs > 0 ? c->opt.block_songs : auto_block_songs(width, n_te, fused, k, n_tr);
   }
+  if (fused && bs > 8192) return fail(MR_E_INVALID, "fused stage 1 needs block_songs <= 8192 (got %d)", bs);
+  if (!wide && k > kMaxTopkLarge && bs > kMaxTopkTile)
+    return fail(MR_E_INVALID, "with topk > %d block_songs must be <= %d (got %d)", kMaxTopkLarge, kMaxTopkTile, bs);
   const int n_tiles = (width + bs - 1) / bs;
   // Per-song / per-user fixed-point tables, computed once on the host with
   // correctly rounded std::sqrt (java.lang.Math.sqrt semantics, MR:147/237).
@@ -2777,45 +2429,62 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const double two_f = std::ldexp(1.0, F);
   std::vector<double> sqrt_c(n_s), sqrt_tr(std::max(1, n_tr)), sqrt_te(n_te);
   std::vector<long long> q_song(n_s);
-  for (int s = 0; s < n_s; ++s) {
-    sqrt_c[s] = std::sqrt((double)d->song_count[s]);
-    q_song[s] = (long long)std::nearbyint(two_f / sqrt_c[s]);
-  }
-  for (int v = 0; v < n_tr; ++v) sqrt_tr[v] = std::sqrt((double)tr_len[v]);
+  mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
+    for (int64_t s2 = a; s2 < b; ++s2) {
+      sqrt_c[s2] = std::sqrt((double)d->song_count[s2]);
+      q_song[s2] = (long long)std::nearbyint(two_f / sqrt_c[s2]);
+    }
+  });
+  mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
+    for (int64_t v = a; v < b; ++v) sqrt_tr[v] = std::sqrt((double)tr_len[v]);
+  });
   for (int u = 0; u < n_te; ++u) sqrt_te[u] = std::sqrt((double)d->te_len[u]);
   // Tile-major train CSR over the shard's songs: for tile t, user v, the
   // tile-local ids of S(v) ∩ [lo + t*bs, lo + (t+1)*bs) live at
   // tsongs[toff[t*n_tr + v] .. toff[t*n_tr + v + 1]) (entries ordered by
   // (tile, user, song)), so neighbouring users' segments share cache lines.
-  const size_t n_tv = pull ? 0 : (size_t)n_tiles * n_tr;
-  std::vector<int32_t> toff(n_tv + 1, 0);
-  for (int v = 0; v < (pull ? 0 : n_tr); ++v)
-    for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {
-      const int s = tr_songs[i];
-      if (s >= lo && s < hi) toff[(size_t)((s - lo) / bs) * n_tr + v + 1]++;
-    }
-  for (size_t i = 0; i < n_tv; ++i) toff[i + 1] += toff[i];
+  // Every user writes only its own (tile, user) slots: parallel over users.
+  const size_t n_tv = (size_t)n_tiles * n_tr;
+  mr_par::buffer<int32_t> toff(n_tv + 1);
+  mr_par::parallel_for((int64_t)n_tv, [&](int64_t a, int64_t b, int) { std::fill(toff.begin() + a, toff.begin() + b, 0); });
+  mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+    for (int64_t w = w0; w < w1; ++w)
+      for (int64_t v = ucut[w]; v < ucut[w + 1]; ++v)
+        for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {
+          const int s2 = tr_songs[i];
+          if (s2 >= lo && s2 < hi) toff[(size_t)((s2 - lo) / bs) * n_tr + v]++;
+        }
+  }, 1, W);
+  const int64_t n_entries = mr_par::exclusive_scan(toff.data(), (int64_t)n_tv);
+  toff[n_tv] = (int32_t)n_entries;
   // padded to whole 8-B words (+1): the wide kernel loads a segment's ids as
   // aligned 4-id words
-  std::vector<uint16_t> tsongs((std::max<int64_t>(1, toff[n_tv]) + 3) / 4 * 4 + 4);
-  {
-    std::vector<int32_t> fill(toff.begin(), toff.end() - 1);
-    for (int v = 0; v < (pull ? 0 : n_tr); ++v)
-      for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {
-        const int s = tr_songs[i];
-        if (s < lo || s >= hi) continue;
-        const int t = (s - lo) / bs;
-        tsongs[fill[(size_t)t * n_tr + v]++] = (uint16_t)(s - lo - t * bs);
+  mr_par::buffer<uint16_t> tsongs((std::max<int64_t>(1, n_entries) + 3) / 4 * 4 + 4);
+  std::fill(tsongs.begin() + n_entries, tsongs.end(), (uint16_t)0);
+  mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+    for (int64_t w = w0; w < w1; ++w)
+      for (int64_t v = ucut[w]; v < ucut[w + 1]; ++v) {
+        int cur_t = -1;
+        int32_t at = 0;
+        for (int64_t i = tr_off[v]; i < tr_off[v + 1]; ++i) {  // songs ascend, so tiles do
+          const int s2 = tr_songs[i];
+          if (s2 < lo || s2 >= hi) continue;
+          const int t = (s2 - lo) / bs;
+          if (t != cur_t) {
+            cur_t = t;
+            at = toff[(size_t)t * n_tr + v];
+          }
+          tsongs[at++] = (uint16_t)(s2 - lo - t * bs);
+        }
       }
-  }
-  // Separate shape: test-user batches so the neighbour lists fit 8 GiB.
+  }, 1, W);
+  trace("tiles");
+  // Separate / wide shapes: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = n_chunks * chunk;
   const size_t budget = (size_t)8 << 30;
-  const int batch = (fused || user) ? n_te
-                    : pull ? std::min(n_te, pull_batch)
-                           : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
+  const int batch = fused ? n_te
+                          : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
                                                                       budget / ((size_t)cap * 12)));
-  const int te_stride = (batch + kPullLanes - 1) / kPullLanes * kPullLanes;
 
   hipStream_t st = c->stream;
   if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(tr_off), (size_t)n_tr + 1, st))) return rc;
@@ -2828,24 +2497,20 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
   if ((rc = dev_upload(c->toff, toff.data(), toff.size(), st))) return rc;
-  if (!fused && !pull && n_chunks > 1) {
-    // Chunk boundaries of every listener list (sorted by train user): the
-    // chunked stage 1 reads its sub-list bounds instead of searching.
-    const int nc1 = n_chunks + 1;
-    std::vector<int32_t> sb((size_t)n_s * nc1);
-    for (int s2 = 0; s2 < n_s; ++s2) {
-      int64_t pos = trs_off[s2];
-      const int64_t end = trs_off[s2 + 1];
-      for (int cc = 0; cc <= n_chunks; ++cc) {
-        const int64_t bound = (int64_t)cc * chunk;
-        while (pos < end && trs_users[pos] < bound) ++pos;
-        sb[(size_t)s2 * nc1 + cc] = (int32_t)pos;
-      }
-    }
-    if ((rc = dev_upload(c->sbound, sb.data(), sb.size(), st))) return rc;
-  }
   if ((rc = dev_upload(c->tsongs, tsongs.data(), tsongs.size(), st))) return rc;
-  if (fused || user) {  // n_tr <= 4096 and bs <= 65536: both halves fit 16 bits
+  if (!fused && n_chunks > 1) {
+    // Chunk boundaries of every listener list (sorted by train user), built on
+    // the device from the uploaded transpose: the chunked stage 1 reads its
+    // sub-list bounds instead of searching (n_s x (n_chunks + 1) ints).
+    const int nc1 = n_chunks + 1;
+    const size_t n_sb = (size_t)n_s * nc1;
+    if ((rc = dev_alloc(c->sbound, n_sb))) return rc;
+    const int grid = (int)std::min<size_t>(8192, (n_sb + 255) / 256);
+    hipLaunchKernelGGL(k_sbound, dim3(grid), dim3(256), 0, st, c->trs_off.p, c->trs_users.p, n_s, nc1, chunk,
+                       c->sbound.p);
+    MR_HIP(hipGetLastError());
+  }
+  if (fused) {  // n_tr <= 4096 and bs <= 65536: both halves fit 16 bits
     std::vector<uint32_t> tpack(tsongs.size(), 0u);
     for (size_t t = 0; t < (size_t)n_tiles; ++t)
       for (int v = 0; v < n_tr; ++v)
@@ -2864,18 +2529,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     }
     if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
     if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
-  }
-  if (pull) {
-    if ((rc = dev_alloc(c->yt, (size_t)std::max(1, n_tr) * te_stride))) return rc;
-    if ((rc = dev_alloc(c->dbg, 1))) return rc;
-    MR_HIP(hipMemsetAsync(c->dbg.p, 0, sizeof(unsigned), st));
-  } else if (!fused && !user) {
+  } else {
     if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
   }
   if (k > 0) {
-    const size_t nc = (size_t)(pull ? te_stride : wide ? batch : n_te) * n_tiles * k;
+    const size_t nc = (size_t)(wide ? batch : n_te) * n_tiles * k;
     if ((rc = dev_alloc(c->cand_key, nc))) return rc;
     if ((rc = dev_alloc(c->cand_song, nc))) return rc;
     if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
@@ -2891,25 +2551,20 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->fused = fused;
   c->shape = shape;
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
-  c->te_stride = te_stride;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
-  c->score_lds = pull ? 0 : wide ? c->wide_lds
-                           : user ? (size_t)user_lds<kWideThreads>(bs, n_tr, k).total
-                                  : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
+  c->score_lds = wide ? c->wide_lds : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
                 c->score_lds);
-  c->nbr_lds = (size_t)align16((pull ? n_tr : chunk) * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
+  c->nbr_lds = (size_t)align16(chunk * 8) + kThreads * 16 + (kThreads + 4 + kWaves) * 4;
   for (int m = 0; m < 2; ++m) {
     MR_HIP(hipFuncSetAttribute((const void*)c->score_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
-    MR_HIP(hipFuncSetAttribute((const void*)c->col_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c->nbr_lds));
   }
-  if ((pull || wide) && k > 0) {
+  if (wide && k > 0) {
     c->merge_lds = (size_t)merge_lds_bytes(k);
     MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->merge_lds));
@@ -2919,6 +2574,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * (batch + 8) * kStampSlots * 8, st));
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
+  trace("upload");
 
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
   c->song_lo = lo; c->song_hi = hi; c->width = width;
@@ -2964,7 +2620,7 @@ int mr_shard_tile_songs(const mr_options* opt, int32_t n_train_users, int32_t n_
   if (n_train_users < 0 || n_test_users <= 0)
     return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d", n_train_users, n_test_users);
   *tile_songs = 0;
-  if (pick_shape(o, n_train_users, n_test_users, false) != kShapeWide || o.topk > kMaxTopkLarge) return MR_OK;
+  if (pick_shape(o, n_train_users, n_test_users) != kShapeWide || o.topk > kMaxTopkLarge) return MR_OK;
   const int chunk = stage1_chunk_for(o, n_train_users);
   const int n_chunks = (std::max(1, n_train_users) + chunk - 1) / chunk;
   *tile_songs = o.block_songs > 0 ? o.block_songs : wide_bmax(o.topk, n_chunks);
@@ -3001,7 +2657,7 @@ int run_model(mr_ctx* c, int model) {
         if (rc) return rc;
       }
       ev = &c->ring[(size_t)c->ring_used * 3];
-      c->ring_has_stage1[c->ring_used] = c->shape != kShapeFused && c->shape != kShapeUser;
+      c->ring_has_stage1[c->ring_used] = c->shape != kShapeFused;
       c->ring_used++;
       MR_HIP(hipEventRecord(ev[0], st));
     }
@@ -3020,52 +2676,6 @@ int run_model(mr_ctx* c, int model) {
                            c->nbr_lds, st, q);
       }
       MR_HIP(hipGetLastError());
-    }
-    if (c->shape == kShapePull) {
-      if (!c->yt.p || (k > 0 && (!c->cand_key.p || !c->top_key.p)))
-        return fail(MR_E_STATE, "pull shape without its buffers");
-      ColParams cp{c->n_tr, user0, c->te_stride, c->opt.frac_bits, c->te_off.p, c->te_songs.p, c->trs_off.p,
-                   c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->yt.p, c->dbg.p,
-                   (long long)c->yt.n};
-      hipLaunchKernelGGL(c->col_kernel[model], dim3(nb), dim3(kThreads), c->nbr_lds, st, cp);
-      MR_HIP(hipGetLastError());
-#ifdef MR_CHECKS
-      MR_HIP(hipStreamSynchronize(st));
-#endif
-      if (timed) MR_HIP(hipEventRecord(ev[1], st));
-      PullParams pp{};
-      pp.user0 = user0; pp.n_users = nb; pp.te_stride = c->te_stride;
-      pp.song_lo = c->song_lo; pp.song_hi = c->song_hi; pp.width = c->width;
-      pp.range = c->block_songs; pp.n_ranges = c->n_tiles;
-      pp.frac_bits = c->opt.frac_bits; pp.topk = k; pp.dense = c->opt.dense;
-      pp.Yt = c->yt.p; pp.trs_off = c->trs_off.p; pp.trs_users = c->trs_users.p; pp.sqrt_c = c->sqrt_c.p;
-      pp.te_off = c->te_off.p; pp.te_songs = c->te_songs.p;
-      pp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p; pp.cand_key = c->cand_key.p; pp.cand_song = c->cand_song.p;
-      pp.dbg = c->dbg.p;
-      pp.n_yt = (long long)c->yt.n; pp.n_trs = (long long)c->trs_users.n; pp.n_te_songs = (long long)c->te_songs.n;
-      pp.n_te_off = (long long)c->te_off.n; pp.n_songs1 = (long long)c->trs_off.n;
-      pp.n_dense = (long long)(c->dense.n / (c->opt.out_dtype == MR_OUT_F64 ? 8 : 4));
-      pp.n_cand = (long long)c->cand_key.n;
-      const int wy = (nb + kWaves * kPullLanes - 1) / (kWaves * kPullLanes);
-      hipLaunchKernelGGL(c->pull_kernel[model], dim3(c->n_tiles, wy), dim3(kThreads), 0, st, pp);
-      MR_HIP(hipGetLastError());
-#ifdef MR_CHECKS
-      MR_HIP(hipStreamSynchronize(st));
-#endif
-      if (k > 0) {
-        MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,
-                       c->top_key.p + (size_t)user0 * k, c->top_song.p + (size_t)user0 * k,
-                       c->top_score.p + (size_t)user0 * k, c->dbg.p, (long long)c->cand_key.n,
-                       (long long)(c->top_key.n - (size_t)user0 * k)};
-        hipLaunchKernelGGL(k_topk_merge, dim3(nb), dim3(kThreads), c->merge_lds, st, mp);
-        MR_HIP(hipGetLastError());
-#ifdef MR_CHECKS
-        MR_HIP(hipStreamSynchronize(st));  // names the faulting kernel in diagnostic runs
-#endif
-      }
-      if (c->win_open) c->win_launches++;
-      if (timed) MR_HIP(hipEventRecord(ev[2], st));
-      continue;
     }
     if (timed) MR_HIP(hipEventRecord(ev[1], st));
     for (int y0 = 0; y0 < nb; y0 += 65528) {
@@ -3086,7 +2696,7 @@ int run_model(mr_ctx* c, int model) {
       sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
-      sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused / user shapes (else null)
+      sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused shape (else null)
 #ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
       sp.te_rng = nullptr;
 #endif
@@ -3101,16 +2711,13 @@ int run_model(mr_ctx* c, int model) {
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       sp.topk_lists = c->opt.topk_lists;
-      if (c->shape == kShapeUser)  // one workgroup per test user, the whole shard
-        hipLaunchKernelGGL(c->score_kernel[model], dim3(ny), dim3(kWideThreads), c->score_lds, st, sp);
-      else
-        hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
-                           c->score_lds, st, sp);
+      hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
+                         c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
       if (wide && k > 0 && c->n_tiles > 1) {  // per-user top-k over the tiles' candidates
         MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,
                        c->top_key.p + (size_t)(user0 + y0) * k, c->top_song.p + (size_t)(user0 + y0) * k,
-                       c->top_score.p + (size_t)(user0 + y0) * k, c->dbg.p, 0, 0};
+                       c->top_score.p + (size_t)(user0 + y0) * k};
         hipLaunchKernelGGL(k_topk_merge, dim3(ny), dim3(kThreads), c->merge_lds, st, mp);
         MR_HIP(hipGetLastError());
       }
@@ -3292,20 +2899,6 @@ int mr_topk_merge_device(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, c
   if (rc) return rc;
   MR_HIP(hipStreamSynchronize(c->stream));
   return MR_OK;
-}
-
-int mr_debug_checks(mr_ctx* c, uint32_t* bits) {
-  if (!c || !bits) return fail(MR_E_INVALID, "null argument");
-#ifndef MR_CHECKS
-  return fail(MR_E_STATE, "library built without -DMR_CHECKS");
-#else
-  *bits = 0;
-  if (!c->dbg.p) return MR_OK;
-  MR_HIP(hipSetDevice(c->opt.device));
-  MR_HIP(hipMemcpyAsync(bits, c->dbg.p, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
-  MR_HIP(hipStreamSynchronize(c->stream));
-  return MR_OK;
-#endif
 }
 
 int mr_debug_stamps(mr_ctx* c, int64_t* out, int64_t n) {

@@ -37,6 +37,63 @@ def user_name(key: int) -> str:
     return "%040x" % key
 
 
+class _Corpus:
+    """Owner of a native mr_corpus: freed when the last array viewing it dies."""
+
+    def __init__(self, L, h):
+        self._L, self._h = L, h
+
+    def __del__(self):  # pragma: no cover - interpreter-driven
+        try:
+            if self._h:
+                self._L.mr_corpus_free(self._h)
+        except Exception:
+            pass
+
+    def view(self, addr, n: int, dt) -> np.ndarray:
+        if n == 0 or not addr:
+            return np.zeros(0, dtype=dt)
+        return np.asarray(_Buffer(self, addr, n, np.dtype(dt)))
+
+    def names(self, kind: int, n: int) -> "_Names":
+        need = ctypes.c_int64()
+        _lib.check(self._L.mr_corpus_names(self._h, kind, None, 0, ctypes.byref(need)), "mr_corpus_names")
+        buf = np.empty(max(1, need.value), dtype=np.uint8)
+        _lib.check(self._L.mr_corpus_names(self._h, kind, buf.ctypes.data_as(ctypes.c_char_p), need.value,
+                                           ctypes.byref(need)), "mr_corpus_names")
+        ends = np.flatnonzero(buf[:need.value] == 10)
+        if ends.size != n:
+            raise RuntimeError(f"mr_corpus_names: {ends.size} names of kind {kind}, expected {n}")
+        return _Names(buf, ends)
+
+
+class _Buffer:
+    """numpy view of native memory that keeps its owner alive (the array's base)."""
+
+    def __init__(self, owner, addr: int, n: int, dt: np.dtype):
+        self._owner = owner
+        self.__array_interface__ = {"shape": (n,), "typestr": dt.str, "data": (addr, False), "version": 3}
+
+
+class _Names:
+    """Names of one kind, newline-separated in one buffer; decoded on access."""
+
+    def __init__(self, buf: np.ndarray, ends: np.ndarray):
+        self._buf, self._ends = buf, ends
+
+    def __len__(self) -> int:
+        return int(self._ends.size)
+
+    def __getitem__(self, i: int) -> str:
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        a = int(self._ends[i - 1]) + 1 if i else 0
+        return self._buf[a:int(self._ends[i])].tobytes().decode()
+
+
 @dataclass
 class Dataset:
     n_train: int
@@ -119,6 +176,8 @@ class Dataset:
     # ---- constructors --------------------------------------------------------
     @staticmethod
     def from_tsv(train_path: str, test_path: str, labels_path: Optional[str] = None) -> "Dataset":
+        """Native ingest (mr_corpus_from_tsv). The arrays are views of the
+        native corpus (no copy), which lives as long as any of them."""
         L = _lib.lib()
         h = ctypes.c_void_p()
         _lib.check(
@@ -126,51 +185,37 @@ class Dataset:
                 os.fsencode(train_path), os.fsencode(test_path),
                 os.fsencode(labels_path) if labels_path else None, ctypes.byref(h)),
             "mr_corpus_from_tsv")
-        try:
-            d = _lib.MrDataset()
-            _lib.check(L.mr_corpus_dataset(h, ctypes.byref(d)), "mr_corpus_dataset")
-            n_tr, n_te, n_s = d.n_train_users, d.n_test_users, d.n_songs
+        owner = _Corpus(L, h)
+        d = _lib.MrDataset()
+        _lib.check(L.mr_corpus_dataset(h, ctypes.byref(d)), "mr_corpus_dataset")
+        n_tr, n_te, n_s = d.n_train_users, d.n_test_users, d.n_songs
 
-            def arr(ptr, n, dt):
-                if n == 0:
-                    return np.zeros(0, dtype=dt)
-                return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt, copy=True)
+        def arr(ptr, n, dt):
+            return owner.view(ctypes.cast(ptr, ctypes.c_void_p).value, n, dt)
 
-            tr_off = arr(d.tr_off, n_tr + 1, np.int64)
-            te_off = arr(d.te_off, n_te + 1, np.int64)
-            lo = ctypes.POINTER(ctypes.c_int64)()
-            ls = ctypes.POINTER(ctypes.c_int32)()
-            nl = ctypes.c_int32()
-            ne = ctypes.c_int32()
-            _lib.check(L.mr_corpus_labels(h, ctypes.byref(lo), ctypes.byref(ls), ctypes.byref(nl), ctypes.byref(ne)),
-                       "mr_corpus_labels")
-            lab_off = arr(lo, n_te + 1, np.int64)
-            def names(kind, n):  # one bulk copy per kind (mr_corpus_names)
-                need = ctypes.c_int64()
-                _lib.check(L.mr_corpus_names(h, kind, None, 0, ctypes.byref(need)), "mr_corpus_names")
-                buf = ctypes.create_string_buffer(max(1, need.value))
-                _lib.check(L.mr_corpus_names(h, kind, buf, need.value, ctypes.byref(need)), "mr_corpus_names")
-                out = buf.raw[:need.value].decode().split("\n")[:-1]
-                if len(out) != n:
-                    raise RuntimeError(f"mr_corpus_names: {len(out)} names of kind {kind}, expected {n}")
-                return out
-
-            names_s = names(0, n_s + ne.value)
-            names_tr = names(1, n_tr)
-            names_te = names(2, n_te)
-            return Dataset(
-                n_train=n_tr, n_test=n_te, n_songs=n_s,
-                tr_off=tr_off, tr_songs=arr(d.tr_songs, int(tr_off[-1]), np.int32),
-                te_off=te_off, te_songs=arr(d.te_songs, int(te_off[-1]), np.int32),
-                song_count=arr(d.song_count, n_s, np.int32),
-                tr_len=arr(d.tr_len, n_tr, np.int32), te_len=arr(d.te_len, n_te, np.int32),
-                lab_off=lab_off, lab_songs=arr(ls, int(lab_off[-1]), np.int32),
-                n_label_songs=nl.value, n_extra_songs=ne.value,
-                song_names=names_s.__getitem__, train_names=names_tr.__getitem__,
-                test_names=names_te.__getitem__,
-            )
-        finally:
-            L.mr_corpus_free(h)
+        tr_off = arr(d.tr_off, n_tr + 1, np.int64)
+        te_off = arr(d.te_off, n_te + 1, np.int64)
+        lo = ctypes.POINTER(ctypes.c_int64)()
+        ls = ctypes.POINTER(ctypes.c_int32)()
+        nl = ctypes.c_int32()
+        ne = ctypes.c_int32()
+        _lib.check(L.mr_corpus_labels(h, ctypes.byref(lo), ctypes.byref(ls), ctypes.byref(nl), ctypes.byref(ne)),
+                   "mr_corpus_labels")
+        lab_off = arr(lo, n_te + 1, np.int64)
+        names_s = owner.names(0, n_s + ne.value)
+        names_tr = owner.names(1, n_tr)
+        names_te = owner.names(2, n_te)
+        return Dataset(
+            n_train=n_tr, n_test=n_te, n_songs=n_s,
+            tr_off=tr_off, tr_songs=arr(d.tr_songs, int(tr_off[-1]), np.int32),
+            te_off=te_off, te_songs=arr(d.te_songs, int(te_off[-1]), np.int32),
+            song_count=arr(d.song_count, n_s, np.int32),
+            tr_len=arr(d.tr_len, n_tr, np.int32), te_len=arr(d.te_len, n_te, np.int32),
+            lab_off=lab_off, lab_songs=arr(ls, int(lab_off[-1]), np.int32),
+            n_label_songs=nl.value, n_extra_songs=ne.value,
+            song_names=names_s.__getitem__, train_names=names_tr.__getitem__,
+            test_names=names_te.__getitem__,
+        )
 
     @staticmethod
     def from_triplets(train_u: np.ndarray, train_s: np.ndarray, test_u: np.ndarray, test_s: np.ndarray,

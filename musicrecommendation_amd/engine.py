@@ -42,7 +42,7 @@ class Engine:
         opt.topk = topk
         opt.dense = 1 if dense else 0
         opt.time_kernels = 1 if time_kernels else 0
-        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4, "user": 5}[stage1]
+        opt.stage1 = _lib.STAGE1[stage1]
         opt.stage1_chunk = stage1_chunk
         opt.train_order = {"auto": 0, "given": 1}[train_order]
         opt.topk_lists = 1 if topk_lists else 0
@@ -66,7 +66,7 @@ class Engine:
         fz, bsz, nt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self._L.mr_launch_info(self._h, ctypes.byref(fz), ctypes.byref(bsz), ctypes.byref(nt)),
                    "mr_launch_info")
-        self.shape = {0: "separate", 1: "fused", 2: "pull", 3: "wide", 4: "user"}[fz.value]
+        self.shape = _lib.SHAPES[fz.value]
         self.fused, self.block_songs, self.n_tiles = self.shape == "fused", bsz.value, nt.value
         b, ch, nch = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self._L.mr_batch_info(self._h, ctypes.byref(b), ctypes.byref(ch), ctypes.byref(nch)),

@@ -47,7 +47,7 @@ class Group:
         opt.out_dtype = {"f32": _lib.MR_OUT_F32, "f64": _lib.MR_OUT_F64}[out_dtype]
         opt.topk = topk
         opt.dense = 1 if dense else 0
-        opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4, "user": 5}[stage1]
+        opt.stage1 = _lib.STAGE1[stage1]
         go = _lib.MrGroupOptions()
         _lib.check(self._L.mr_group_options_default(ctypes.byref(go)), "mr_group_options_default")
         go.n_song_shards, go.n_user_blocks = song_shards, user_blocks

@@ -69,7 +69,7 @@ def shard_tile(n_train: int, n_test: int, *, topk: int = 10, stage1: str = "auto
     _lib.check(L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
     opt.topk = topk
     opt.block_songs = block_songs
-    opt.stage1 = {"auto": 0, "fused": 1, "separate": 2, "pull": 3, "wide": 4, "user": 5}[stage1]
+    opt.stage1 = _lib.STAGE1[stage1]
     opt.stage1_chunk = stage1_chunk
     out = ctypes.c_int32()
     _lib.check(L.mr_shard_tile_songs(ctypes.byref(opt), int(n_train), int(n_test), ctypes.byref(out)),

@@ -56,6 +56,49 @@ class Triplets:
     def n_songs(self) -> int:
         return int(np.unique(np.concatenate([self.train_s, self.test_s])).size)
 
+    def write_tsv(self, train_path: str, test_path: str, labels_path: str) -> int:
+        """The three reference-format files (``user\tsong\t1`` lines in row
+        order, names as dataset.user_name / song_name), written with numpy in
+        blocks of rows: the full-scale files (48M lines, ~3 GB) in seconds.
+        Returns the bytes written."""
+        total = 0
+        for path, u, s in ((train_path, self.train_u, self.train_s), (test_path, self.test_u, self.test_s),
+                           (labels_path, self.label_u, self.label_s)):
+            total += _write_triplet_file(path, u, s)
+        return total
+
+
+def _hex_names(keys: np.ndarray, prefix: bytes, width: int, upper: bool) -> np.ndarray:
+    """Rows of fixed-width names prefix + hex(key) (dataset.user_name: 40 lower-case
+    hex digits; song_name: "SO" + 16 upper-case), one uint8 row per key."""
+    digits = np.frombuffer(b"0123456789ABCDEF" if upper else b"0123456789abcdef", dtype=np.uint8)
+    out = np.empty((keys.size, len(prefix) + width), dtype=np.uint8)
+    if prefix:
+        out[:, :len(prefix)] = np.frombuffer(prefix, dtype=np.uint8)
+    k = keys.astype(np.uint64)
+    for i in range(width):
+        out[:, len(prefix) + width - 1 - i] = digits[((k >> np.uint64(4 * i)) & np.uint64(15)).astype(np.intp)]
+    return out
+
+
+def _write_triplet_file(path: str, u: np.ndarray, s: np.ndarray, block: int = 1 << 22) -> int:
+    uk, ui = np.unique(u, return_inverse=True)
+    sk, si = np.unique(s, return_inverse=True)
+    un = _hex_names(uk, b"", 40, False)
+    sn = _hex_names(sk, b"SO", 16, True)
+    wu, ws = un.shape[1], sn.shape[1]
+    line = wu + ws + 4  # user \t song \t 1 \n
+    with open(path, "wb") as f:
+        for a in range(0, u.size, block):
+            b = min(u.size, a + block)
+            rows = np.empty((b - a, line), dtype=np.uint8)
+            rows[:, :wu] = un[ui[a:b]]
+            rows[:, wu] = 9
+            rows[:, wu + 1:wu + 1 + ws] = sn[si[a:b]]
+            rows[:, wu + 1 + ws:] = np.frombuffer(b"\t1\n", dtype=np.uint8)
+            rows.tofile(f)
+    return int(u.size) * line
+
 
 def _user_songs(rng: np.random.Generator, cdf: np.ndarray, perm: np.ndarray) -> np.ndarray:
     """One user's history: length max(10, round(lognormal(3.51, 0.86))), distinct

@@ -13,7 +13,7 @@ from musicrecommendation_amd.engine import Engine  # noqa: E402
 model = sys.argv[1] if len(sys.argv) > 1 else "ibm"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 400
 ds = synth.config("c2").dataset()
-shapes = (("fused", (256, 512, 768, 1024, 2048)), ("user", (0,)))
+shapes = (("fused", (256, 512, 768, 1024, 2048)),)
 if os.environ.get("BS"):
     shapes = (("fused", tuple(int(x) for x in os.environ["BS"].split())),)
 for stage1, bss in shapes:

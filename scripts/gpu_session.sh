@@ -25,8 +25,9 @@ run() {  # name limit cmd...
 }
 
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/gpu.txt" || true
-case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;; esac
+case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread ;; esac
 case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
+case ",$STEPS," in *,ingest,*) MR_INGEST_TRACE=1 MR_LOAD_TRACE=1 run ingest_c4 900 python -u scripts/ingest_probe.py --config c4 --load --reps 3 --out "$OUT/ingest_c4.json" ;; esac
 case ",$STEPS," in *,bench,*) run bench 600 python bench.py ;; esac
 case ",$STEPS," in *,prof,*)
   export TMPDIR=/tmp

@@ -10,7 +10,7 @@ from musicrecommendation_amd.engine import Engine  # noqa: E402
 for n_tr, n_te in ((500, 10), (500, 32), (500, 64), (500, 128), (500, 256), (2000, 10), (2000, 32), (2000, 100), (2000, 1000), (5000, 1000), (10000, 300), (10000, 1000), (16000, 2000)):
     ds = synth.generate_bulk(n_tr, n_te, 3).dataset()
     row = [f"{n_tr:6d}/{n_te:5d} songs {ds.n_songs:6d}"]
-    for shape in ("fused", "separate", "pull", "wide", "user"):
+    for shape in ("fused", "separate", "wide"):
         try:
             with Engine(ds, topk=10, stage1=shape) as e:
                 e.run("ibm")

@@ -8,6 +8,8 @@ Bars (BASELINE.json north_star):
     measured errors are ~1e-8 (fixed-point rounding, F = 32);
   * identical top-k song lists for every tile size and shard count.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -152,67 +154,6 @@ def test_large_train_set_exact(model):
     assert np.array_equal(ms, ts) and np.array_equal(mk, tk)
 
 
-# ---- pull shape (dense neighbourhoods): Yt columns + per-song row gathers ----
-@pytest.mark.parametrize("block", [256, 512, 2048, 16384])
-@pytest.mark.parametrize("model", MODELS)
-@pytest.mark.parametrize("name", ["tiny", "small"])
-def test_pull_ranges_bit_identical(name, model, block):
-    ds, z = synth_fixture(name)
-    with Engine(ds, stage1="pull", block_songs=block) as e:
-        assert e.shape == "pull" and e.block_songs == block
-    got, songs = check_exact(ds, model, stage1="pull", block_songs=block)
-    topk_consistent(songs, z[model], 10)
-
-
-@pytest.mark.parametrize("k", [1, 7, 16])
-@pytest.mark.parametrize("model", MODELS)
-def test_pull_topk_sizes(k, model):
-    ds, _ = synth_fixture("small")
-    check_exact(ds, model, k=k, stage1="pull")
-    with Engine(ds, stage1="pull", topk=k, dense=False) as e:
-        e.run(model)
-        songs, _, keys = e.topk()
-    _, ts, tk = native.fp_model(ds, model, k=k, dense=False)
-    assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
-    with Engine(ds, stage1="pull", topk=0, out_dtype="f64") as e:
-        assert np.array_equal(e.score_dense(model), native.fp_model(ds, model)[0], equal_nan=True)
-
-
-def test_pull_limits_and_kats():
-    ds, _ = synth_fixture("small")
-    with pytest.raises(_lib.EngineError):
-        Engine(ds, stage1="pull", topk=17)
-    for key in (None, "dup"):
-        K = kat() if key is None else kat()[key]
-        d = dataset_from_lines(K["train"], K["test"], K["labels"])
-        for model in MODELS:
-            got, _ = check_exact(d, model, k=4, stage1="pull")
-            assert rel_err(got, dense_from_pairs(d, K["expected"][model])) < 1e-9
-    train = ["A\ts1\t1", "A\ts2\t1", "B\ts2\t1"]
-    test = ["X\ts9\t1", "Y\ts1\t1"]
-    d = dataset_from_lines(train, test, ["X\ts1\t1"])
-    for model in MODELS:
-        _, songs = check_exact(d, model, k=3, stage1="pull")
-        assert songs[0].tolist() == [0, 1, -1]
-
-
-@pytest.mark.parametrize("model", MODELS)
-def test_pull_song_shards(model):
-    ds = synth.config("c2").dataset()
-    _, fs = check_exact(ds, model)
-    ss, kk = [], []
-    for lo, hi in song_shards(ds, 3):
-        with Engine(ds, out_dtype="f64", song_lo=lo, song_hi=hi, stage1="pull") as e:
-            e.run(model)
-            s, _, k = e.topk()
-        exp, ts, tk = native.fp_model(ds, model, song_lo=lo, song_hi=hi, k=10, dense=False)
-        assert np.array_equal(s, ts) and np.array_equal(k, tk)
-        ss.append(s)
-        kk.append(k)
-    ms, _msc, _mk = merge_topk_host(np.stack(ss), np.stack(kk))
-    assert np.array_equal(ms, fs)
-
-
 def test_launch_shape_selection():
     ds, _ = synth_fixture("small")
     with Engine(ds) as e:
@@ -232,6 +173,13 @@ def test_launch_shape_selection():
         assert e.shape == "fused"
     with Engine(c2, topk=17) as e:
         assert e.shape == "fused"
+    # round-2 shapes 3 (pull) and 5 (user) are gone: rejected, not silently mapped
+    for code in (3, 5):
+        o = _lib.MrOptions()
+        _lib.check(_lib.lib().mr_options_default(ctypes.byref(o)), "defaults")
+        o.stage1 = code
+        h = ctypes.c_void_p()
+        assert _lib.lib().mr_create(ctypes.byref(o), ctypes.byref(h)) == _lib.MR_E_INVALID
 
 
 @pytest.mark.parametrize("frac_bits", [16, 24, 40])
@@ -259,7 +207,7 @@ def test_topk_only_mode():
     assert np.array_equal(songs, ts) and np.array_equal(keys, tk)
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "user"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "wide"])
 @pytest.mark.parametrize("name", ["c1", "c2"])
 @pytest.mark.parametrize("model", MODELS)
 def test_named_configs_exact(name, model, stage1):
@@ -406,7 +354,7 @@ def test_errors_are_codes_not_aborts():
         assert ei.value.code == _lib.MR_E_STATE
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide", "user"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "wide"])
 def test_train_order_does_not_change_results(stage1):
     """mr_load renumbers train users by history length (load balance); the
     caller's order gives bit-identical scores and lists."""
@@ -421,7 +369,7 @@ def test_train_order_does_not_change_results(stage1):
         assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][3], out[1][3])
 
 
-@pytest.mark.parametrize("stage1", ["fused", "separate", "pull", "wide", "user"])
+@pytest.mark.parametrize("stage1", ["fused", "separate", "wide"])
 def test_degenerate_inputs(stage1):
     """Edge cases of the reference's inputs, every launch shape, exact vs the
     oracle: no train users at all (every score 0, MR:159-166 / MR:249-257 sum
@@ -442,32 +390,7 @@ def test_degenerate_inputs(stage1):
                 assert (songs[0] == -1).all()  # X heard every song: no candidate
 
 
-@pytest.mark.parametrize("k", [1, 10, 16])
-@pytest.mark.parametrize("model", MODELS)
-def test_user_shape(model, k):
-    """One workgroup per test user over the whole shard (stage 1 fused, no
-    merge): fixtures, C2 and a song shard of it, f64 and f32; the limits fail loudly."""
-    c2 = synth.config("c2", n_test=13).dataset()
-    for ds in (synth_fixture("tiny")[0], synth_fixture("small")[0], c2):
-        check_exact(ds, model, k=k, stage1="user")
-    check_exact(c2, model, k=k, stage1="user", song_lo=1000, song_hi=9000)
-    with Engine(c2, topk=k, stage1="user") as e:
-        assert e.shape == "user" and e.n_tiles == 1
-        g32 = e.score_dense(model)
-    exp, _, _ = native.fp_model(c2, model, k=1)
-    assert np.array_equal(g32, exp.astype(np.float32), equal_nan=True)
-    with Engine(c2, topk=0, out_dtype="f64", stage1="user") as e:  # dense model only
-        assert np.array_equal(e.score_dense(model), exp, equal_nan=True)
-    with pytest.raises(_lib.EngineError):
-        Engine(c2, stage1="user", topk=17)
-    with pytest.raises(_lib.EngineError):
-        Engine(c2, stage1="user", block_songs=256)
-    big = synth.generate_bulk(3000, 4, 5).dataset()  # > 20k songs: the tile does not fit the LDS
-    with pytest.raises(_lib.EngineError):
-        Engine(big, stage1="user")
-
-
-@pytest.mark.parametrize("stage1", ["wide", "user"])
+@pytest.mark.parametrize("stage1", ["wide"])
 @pytest.mark.parametrize("model", MODELS)
 def test_topk_paths_identical(model, stage1):
     """The threshold top-k and the per-thread-list top-k give the same lists,
