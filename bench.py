@@ -209,7 +209,8 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     from musicrecommendation_amd.sharding import layout_2d, shard_tile, song_shards, user_blocks
 
     n_tr, n_te, _seed = synth.BULK_CONFIGS["c5"]
-    full = synth.config("c5").dataset()
+    trip = synth.config("c5")
+    full = trip.dataset()
     gs, gu = layout_2d(world, song_groups_for(args, world))
     a, b = user_blocks(full.n_test, gu)[rank // gs]
     lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu))[rank % gs]
@@ -283,6 +284,8 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
             "cpu_baseline": (cpu_baseline_twohop(full, "ibm", args.cpu_baseline_seconds)
                              if world == 1 and not args.no_cpu_baseline else None),
         }
+        if world == 1 and not args.no_e2e:
+            line["end_to_end"] = end_to_end_bulk(trip, "ibm")
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
@@ -339,6 +342,121 @@ def end_to_end(ds, model: str, reps: int = 3):
                     "D2H of the dense fp32 model; median of 3 (value excludes all of this but the kernels)"}
 
 
+def north_star(args, world: int, rank: int, local: int):
+    """The north star's layout at this N (BASELINE.json: "item-item similarity
+    partitions by song-id range across the 8 GPUs ... with a single RCCL
+    all-gather of per-test-user partial scores"): C4 = the full Taste-Profile
+    shape (1,009,318 train / 10,000 test / 384,546 songs, top-10), strong
+    scaling over the fixed test set in the 2-D layout of sharding.ShardScorer —
+    G_s song shards (2 when N is even, else N) x N / G_s test-user blocks; the
+    song shards of a block exchange their top-k record blocks with ONE
+    all-gather (RCCL) and merge them on the device (distributed.scala:477-479's
+    song partition, :468-470's user partition). Every rank runs this; returns
+    the block for rank 0's line (None elsewhere)."""
+    from musicrecommendation_amd.sharding import ShardScorer
+
+    t0 = time.perf_counter()
+    full = synth.config("c4").dataset()
+    gen_s = time.perf_counter() - t0
+    gs = 1 if world == 1 else (2 if world % 2 == 0 else world)
+    t0 = time.perf_counter()
+    scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32")
+    load_s = time.perf_counter() - t0
+
+    def timed(fn, k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        scorer.sync()
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        scorer.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item())
+
+    for _ in range(args.ns_warmup):
+        scorer.step(args.model)
+    step_s = timed(lambda: scorer.step(args.model), args.ns_steps)
+    exch_s = timed(scorer.exchange, args.ns_steps) if scorer.gs > 1 else 0.0
+    pairs_rank = torch.tensor([float(scorer.pairs())], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(pairs_rank, op=dist.ReduceOp.SUM)
+    pairs = float(pairs_rank.item())
+    out = None
+    if rank == 0:
+        ms = step_s / args.ns_steps * 1e3
+        out = {
+            "workload": f"c4: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} {full.n_train} train / "
+                        f"{full.n_test} test / {full.n_songs} songs, top-10 only",
+            "layout": f"songs{scorer.gs}xusers{scorer.gu}", "song_shards": scorer.gs, "user_blocks": scorer.gu,
+            "value": pairs * args.ns_steps / step_s, "unit": "pairs/s", "scaling": "strong",
+            "pairs_per_step": pairs, "steps": args.ns_steps, "warmup": args.ns_warmup,
+            "ms_per_step": ms,  # slowest rank: max over ranks of the barrier-bracketed window
+            "exchange_ms_per_step": exch_s / args.ns_steps * 1e3 if scorer.gs > 1 else 0.0,
+            "exchange": ("one all_gather_into_tensor of the top-k record blocks (int64 keys + int32 songs) per "
+                         "step inside each user block, then k_topk_merge on the device" if scorer.gs > 1 else
+                         "none (one song shard: no exchange)"),
+            "allgather_bytes_per_rank": scorer.gs * scorer.rec_bytes if scorer.gs > 1 else 0,
+            "record_bytes": scorer.rec_bytes,
+            "process_group": {"backend": dist.get_backend() if world > 1 else None,
+                              "world_size": dist.get_world_size() if world > 1 else 1,
+                              "block_group_size": dist.get_world_size(scorer.group) if world > 1 else 1},
+            "setup_s": {"dataset": gen_s, "shard_load": load_s},
+            "note": "strong scaling: the N=1 line runs the whole C4 step on one GPU; compare ms_per_step across N",
+        }
+    scorer.engine.close()
+    return out
+
+
+def end_to_end_bulk(trip, model: str, reps: int = 2, k: int = 10):
+    """Full-scale configs (C4/C5), one GPU, wall clock: the reference's whole
+    call chain at the size the native ingest exists for — ingest of the three
+    TSV files (48.4M rows at C4; ≙ the MusicRecommender constructor,
+    MR:26-91) -> mr_load (host index build + H2D) -> mr_run -> D2H of the
+    top-k lists (the dense model is 15 GB at C4: top-k output, SURVEY.md §7
+    hard part 4). The files are written once beforehand (untimed)."""
+    import tempfile
+
+    from musicrecommendation_amd.dataset import Dataset
+
+    rows = []
+    with tempfile.TemporaryDirectory() as td:
+        paths = [os.path.join(td, n) for n in ("train.txt", "test.txt", "labels.txt")]
+        t0 = time.perf_counter()
+        nbytes = trip.write_tsv(*paths)
+        write_s = time.perf_counter() - t0
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d2 = Dataset.from_tsv(*paths)
+            t1 = time.perf_counter()
+            e = Engine(d2, device=torch.cuda.current_device(), topk=k, dense=False)
+            t2 = time.perf_counter()
+            e.run(model)
+            e.sync()
+            t3 = time.perf_counter()
+            songs, _sc, _k = e.topk()
+            t4 = time.perf_counter()
+            e.close()
+            rows.append((t4 - t0, t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+            del d2
+    rows.sort()
+    tot, ing, load, run, d2h = rows[len(rows) // 2]
+    n_rows = int(trip.train_u.size + trip.test_u.size + trip.label_u.size)
+    return {"ms": tot * 1e3, "rows": n_rows, "tsv_bytes": nbytes,
+            "breakdown_ms": {"ingest_tsv": ing * 1e3, "mr_load_index_h2d": load * 1e3, "mr_run": run * 1e3,
+                             "d2h_topk": d2h * 1e3},
+            "ingest_rows_per_s": n_rows / ing, "host_cores": host_cores()["threads"],
+            "note": f"wall clock, one GPU, median of {reps}: native TSV ingest (mr_corpus_from_tsv) + mr_load + "
+                    f"mr_run + D2H of the top-{k} lists; files written beforehand in {write_s:.1f} s (untimed)"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -351,6 +469,10 @@ def main() -> None:
                          "top-k lists (north star), or the 2-D product of both (--song-groups)")
     ap.add_argument("--song-groups", type=int, default=0, help="2d: song shards per user block")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (ingest + H2D + D2H) timing")
+    ap.add_argument("--no-north-star", action="store_true",
+                    help="skip the nested C4 2-D layout block (north_star) of the C2 line")
+    ap.add_argument("--ns-steps", type=int, default=5, help="timed steps of the north_star block")
+    ap.add_argument("--ns-warmup", type=int, default=2, help="warmup steps of the north_star block")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
@@ -427,7 +549,8 @@ def main() -> None:
         # fixed test set; small configs: weak, 10 test users per GPU in total.
         from musicrecommendation_amd.sharding import ShardScorer
 
-        full = synth.config(args.config, n_test=None if bulk else n_te * world).dataset()
+        trip = synth.config(args.config, n_test=None if bulk else n_te * world)
+        full = trip.dataset()
         scorer = ShardScorer(full, rank, world, local, song_groups=song_groups_for(args, world), topk=10,
                              out_dtype="f32", dense=dense_out, stage1=args.stage1, block_songs=args.block_songs)
         eng = scorer.engine
@@ -485,6 +608,9 @@ def main() -> None:
     else:
         elapsed_max, pairs_all = elapsed, pairs_total_rank
 
+    ns = None
+    if args.config == "c2" and not args.no_north_star:  # every rank (collectives inside)
+        ns = north_star(args, world, rank, local)
     if rank == 0:
         value = pairs_all / elapsed_max
         ab_stage = algorithmic_bytes(ds, 4 if dense_out else 0, 10)
@@ -591,6 +717,10 @@ def main() -> None:
             line["cpu_baseline"] = None
         if world == 1 and not bulk and not args.no_e2e:
             line["end_to_end"] = end_to_end(ds, args.model)
+        if world == 1 and bulk and not args.no_e2e:
+            line["end_to_end"] = end_to_end_bulk(trip, args.model)
+        if ns is not None:
+            line["north_star"] = ns
         print(json.dumps(line), flush=True)
     for e in engines:
         e.close()

@@ -246,6 +246,20 @@ int mr_topk_merge_device(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k,
 int mr_topk_merge_device_async(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
                                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out);
 
+/*
+ * The exchange as ONE collective: a shard's top-k lists travel as one record
+ * block — n_te*k int64 keys at byte 0, then n_te*k int32 songs at byte
+ * 8*n_te*k, padded to *rec_bytes (a multiple of 16) — so a song-sharded run
+ * all-gathers G blocks in a single call (the north star's "single RCCL
+ * all-gather", distributed.scala:477-479) instead of one per array.
+ * mr_copy_topk_device(_async)(ctx, block + 8*n_te*k, block) fills such a block;
+ * mr_topk_merge_records_async merges G gathered blocks (stride rec_bytes) on
+ * the context stream, like mr_topk_merge_device_async.
+ */
+int mr_topk_record_bytes(int32_t n_te, int32_t k, int64_t* rec_bytes);
+int mr_topk_merge_records_async(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int32_t k, const void* records,
+                                int64_t rec_bytes, int32_t* songs_out, int64_t* keys_out, double* scores_out);
+
 /* ---- combination models and evaluation on the device (MR:317-481, MR:521-639) ----
  * Over dense models of the context's shard (device pointers, n_te x width of
  * the context's out_dtype, NaN = no pair), e.g. filled by mr_run_into. Pairs
@@ -318,12 +332,15 @@ const char* mr_last_error(void);
  * with ONE all-gather and merge them by (key desc, song asc): the results are
  * bit-identical to one context (fixed-point keys) for every layout.
  * Transports: MR_TRANSPORT_RCCL — every context on its own device, one RCCL
- * communicator per user block (ncclCommInitAll, owned by the group; librccl is
- * loaded on first use), ncclAllGather under ncclGroupStart/End on the
- * contexts' streams, the merge on every device; MR_TRANSPORT_COPY — every
- * context on ONE device (logical shards), the block's first context gathers
- * with device copies and merges. AUTO = RCCL when the contexts span >= 2
- * devices. A group is driven by one host thread; calls are synchronous unless
+ * communicator per user block (ncclCommInitAll, owned by the group; librccl —
+ * or the library named by the environment variable MR_RCCL_LIB — is loaded on
+ * first use), ONE ncclAllGather of the top-k record blocks per context under
+ * ncclGroupStart/End on the contexts' streams, the merge on every device;
+ * MR_TRANSPORT_COPY — every context on ONE device (logical shards), the
+ * block's first context gathers the record blocks with device copies and
+ * merges. AUTO = RCCL when the contexts span >= 2 devices. RCCL needs one
+ * distinct device per context (MR_E_INVALID otherwise) unless MR_RCCL_LIB
+ * names a library that accepts shared devices (the test fake). A group is driven by one host thread; calls are synchronous unless
  * stated. */
 #define MR_TRANSPORT_AUTO 0
 #define MR_TRANSPORT_COPY 1
@@ -352,7 +369,8 @@ int mr_group_options_default(mr_group_options* gopt);
 /* opt: the contexts' options (song_lo/song_hi must be 0: the group sets them). */
 int mr_group_create(const mr_options* opt, const mr_group_options* gopt, mr_group** out);
 int mr_group_destroy(mr_group* g);
-/* Split the dataset (shards, user blocks) and load every context (in parallel). */
+/* Validate the dataset as mr_load does, split it (shards, user blocks) and load
+ * every context (in parallel). A reload frees the previous load first. */
 int mr_group_load(mr_group* g, const mr_dataset* d);
 /* Geometry of context i after mr_group_load: songs [*song_lo, *song_hi), test
  * users [*user_lo, *user_hi), device. */

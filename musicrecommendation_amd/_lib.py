@@ -140,6 +140,9 @@ SIGNATURES = {
     "mr_copy_topk_device_async": (c_int, [c_void_p, c_void_p, c_void_p]),
     "mr_topk_merge_device_async": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p]),
+    "mr_topk_record_bytes": (c_int, [c_int32, c_int32, POINTER(c_int64)]),
+    "mr_topk_merge_records_async": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int64, c_void_p, c_void_p,
+                                            c_void_p]),
     "mr_topk_merge_host": (c_int, [c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_topk_merge_device": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),

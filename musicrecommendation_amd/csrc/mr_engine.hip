@@ -1839,17 +1839,23 @@ constexpr long long kWideMinUserPairs = 100000;
 
 // ---------------------------------------------------------------------------
 // Top-k merge over lists (exchange step after a song-shard all-gather).
-// Element (u, l, r) of the input sits at u*user_stride + l*list_stride + r.
+// Element (u, l, r) of the input: key at keys[u*user_stride + l*list_stride_k +
+// r], song at songs[u*user_stride + l*list_stride_s + r] (the strides differ
+// for gathered record blocks: keys and songs of one shard in one block).
 // ---------------------------------------------------------------------------
 struct MergeParams {
   int n_lists, k_in, k_out;
-  long long user_stride, list_stride;
+  long long user_stride, list_stride_k, list_stride_s;
   const long long* keys;
   const int* songs;
   long long* out_keys;    // [n_users][k_out]
   int* out_songs;
   double* out_scores;     // may be null
 };
+
+// Bytes of one shard's top-k record block: n int64 keys then n int32 songs,
+// padded to 16 B (the block stride of a gathered exchange buffer).
+inline int64_t topk_record_bytes(size_t n) { return (int64_t)((12 * n + 15) / 16 * 16); }
 
 __host__ __device__ inline int merge_lds_bytes(int k) {
   return align16(merge_lists_per_pass(k) * k * 12) + align16(kMaxTopK * 12);
@@ -1873,9 +1879,8 @@ __global__ __launch_bounds__(kThreads) void k_topk_merge(MergeParams p) {
     for (int i = tid; i < nl * k; i += kThreads) {
       const int l = done + i / k, r = i - (i / k) * k;
       const bool in = r < p.k_in;
-      const size_t src = (size_t)l * p.list_stride + r;
-      mk[off * k + i] = in ? keys[src] : kKeyNone;
-      ms[off * k + i] = in ? songs[src] : -1;
+      mk[off * k + i] = in ? keys[(size_t)l * p.list_stride_k + r] : kKeyNone;
+      ms[off * k + i] = in ? songs[(size_t)l * p.list_stride_s + r] : -1;
     }
     for (int i = tid; i < off * k; i += kThreads) {
       mk[i] = fk[i];
@@ -1923,10 +1928,12 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  bool own = true;  // false: a view into another buffer's allocation
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && own) (void)hipFree(p);
     p = nullptr;
     n = 0;
+    own = true;
   }
 };
 
@@ -2173,6 +2180,70 @@ int wide_bmax(int k, int n_chunks) {
 
 }  // namespace
 
+// Every input check of mr_load (sizes, CSR shapes, sorted rows, id ranges,
+// duplicate-counting lengths, song counts), in parallel; the distinct train
+// listeners per song come back in *col_tr.
+static int check_dataset(const mr_dataset* d, std::vector<int32_t>& col_tr) {
+  mr_par::PhaseTrace trace("MR_LOAD_TRACE", "mr_load");
+  const int n_tr = d->n_train_users, n_te = d->n_test_users, n_s = d->n_songs;
+  if (n_tr < 0 || n_te <= 0 || n_s <= 0)
+    return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d n_songs=%d", n_tr, n_te, n_s);
+  if (n_tr > kMaxChunks * kStage1Chunk)
+    return fail(MR_E_INVALID, "n_train_users=%d exceeds the stage-1 limit %d of this build", n_tr,
+                kMaxChunks * kStage1Chunk);
+  int rc;
+  if ((rc = validate_csr("train user->songs", n_tr, n_s, d->tr_off, d->tr_songs))) return rc;
+  if ((rc = validate_csr("test user->songs", n_te, n_s, d->te_off, d->te_songs))) return rc;
+  if (!d->song_count || !d->tr_len || !d->te_len) return fail(MR_E_INVALID, "null count arrays");
+  {  // lengths count duplicates: >= the distinct count, and nobody is empty (MR:44-46)
+    const int64_t v = first_bad(n_tr, [&](int64_t v) {
+      const int64_t deg = d->tr_off[v + 1] - d->tr_off[v];
+      return deg <= 0 || d->tr_len[v] < deg;
+    });
+    if (v >= 0)
+      return fail(MR_E_INVALID, "train user %d: %lld distinct songs but length %d", (int)v,
+                  (long long)(d->tr_off[v + 1] - d->tr_off[v]), d->tr_len[v]);
+    const int64_t u = first_bad(n_te, [&](int64_t u) {
+      const int64_t deg = d->te_off[u + 1] - d->te_off[u];
+      return deg <= 0 || d->te_len[u] < deg;
+    });
+    if (u >= 0)
+      return fail(MR_E_INVALID, "test user %d: %lld distinct songs but length %d", (int)u,
+                  (long long)(d->te_off[u + 1] - d->te_off[u]), d->te_len[u]);
+  }
+  const int64_t nnz_tr = d->tr_off[n_tr];
+  // Workers of the bulk passes: ranges of users with about equal entries.
+  const int W = (int)std::max<int64_t>(1, std::min<int64_t>(mr_par::usable_cores(), nnz_tr >> 18));
+  // Distinct listeners per song: train (per-worker histograms) and test.
+  col_tr.assign(n_s, 0);
+  std::vector<int32_t> col_te(n_s, 0);
+  {
+    std::vector<std::vector<int32_t>> h(W);
+    const std::vector<int64_t> cut = weighted_cuts(d->tr_off, n_tr, W);
+    mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
+      for (int64_t w = w0; w < w1; ++w) {
+        h[w].assign(n_s, 0);
+        for (int64_t i = d->tr_off[cut[w]]; i < d->tr_off[cut[w + 1]]; ++i) h[w][d->tr_songs[i]]++;
+      }
+    }, 1, W);
+    mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
+      for (int w = 0; w < W; ++w)
+        for (int64_t s2 = a; s2 < b; ++s2) col_tr[s2] += h[w][s2];
+    }, 4096);
+  }
+  for (int64_t i = 0; i < d->te_off[n_te]; ++i) col_te[d->te_songs[i]]++;
+  {
+    const int64_t s_bad = first_bad(n_s, [&](int64_t s2) {
+      return d->song_count[s2] < col_tr[s2] + col_te[s2] || d->song_count[s2] <= 0;
+    });
+    if (s_bad >= 0)
+      return fail(MR_E_INVALID, "song %d: count %d below its %d distinct listeners (or zero)", (int)s_bad,
+                  d->song_count[s_bad], col_tr[s_bad] + col_te[s_bad]);
+  }
+  trace("validate");
+  return MR_OK;
+}
+
 extern "C" {
 
 const char* mr_last_error(void) { return g_err.c_str(); }
@@ -2268,60 +2339,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->ring_used = 0;
   c->release_data();
   const int n_tr = d->n_train_users, n_te = d->n_test_users, n_s = d->n_songs;
-  if (n_tr < 0 || n_te <= 0 || n_s <= 0)
-    return fail(MR_E_INVALID, "bad sizes: n_train_users=%d n_test_users=%d n_songs=%d", n_tr, n_te, n_s);
-  if (n_tr > kMaxChunks * kStage1Chunk)
-    return fail(MR_E_INVALID, "n_train_users=%d exceeds the stage-1 limit %d of this build", n_tr,
-                kMaxChunks * kStage1Chunk);
+  std::vector<int32_t> col_tr;
   int rc;
-  if ((rc = validate_csr("train user->songs", n_tr, n_s, d->tr_off, d->tr_songs))) return rc;
-  if ((rc = validate_csr("test user->songs", n_te, n_s, d->te_off, d->te_songs))) return rc;
-  if (!d->song_count || !d->tr_len || !d->te_len) return fail(MR_E_INVALID, "null count arrays");
-  {  // lengths count duplicates: >= the distinct count, and nobody is empty (MR:44-46)
-    const int64_t v = first_bad(n_tr, [&](int64_t v) {
-      const int64_t deg = d->tr_off[v + 1] - d->tr_off[v];
-      return deg <= 0 || d->tr_len[v] < deg;
-    });
-    if (v >= 0)
-      return fail(MR_E_INVALID, "train user %d: %lld distinct songs but length %d", (int)v,
-                  (long long)(d->tr_off[v + 1] - d->tr_off[v]), d->tr_len[v]);
-    const int64_t u = first_bad(n_te, [&](int64_t u) {
-      const int64_t deg = d->te_off[u + 1] - d->te_off[u];
-      return deg <= 0 || d->te_len[u] < deg;
-    });
-    if (u >= 0)
-      return fail(MR_E_INVALID, "test user %d: %lld distinct songs but length %d", (int)u,
-                  (long long)(d->te_off[u + 1] - d->te_off[u]), d->te_len[u]);
-  }
-  trace("validate");
+  if ((rc = check_dataset(d, col_tr))) return rc;
   const int64_t nnz_tr = d->tr_off[n_tr];
-  // Workers of the bulk passes: ranges of users with about equal entries.
   const int W = (int)std::max<int64_t>(1, std::min<int64_t>(mr_par::usable_cores(), nnz_tr >> 18));
-  // Distinct listeners per song: train (per-worker histograms) and test.
-  std::vector<int32_t> col_tr(n_s, 0), col_te(n_s, 0);
-  {
-    std::vector<std::vector<int32_t>> h(W);
-    const std::vector<int64_t> cut = weighted_cuts(d->tr_off, n_tr, W);
-    mr_par::parallel_for(W, [&](int64_t w0, int64_t w1, int) {
-      for (int64_t w = w0; w < w1; ++w) {
-        h[w].assign(n_s, 0);
-        for (int64_t i = d->tr_off[cut[w]]; i < d->tr_off[cut[w + 1]]; ++i) h[w][d->tr_songs[i]]++;
-      }
-    }, 1, W);
-    mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
-      for (int w = 0; w < W; ++w)
-        for (int64_t s2 = a; s2 < b; ++s2) col_tr[s2] += h[w][s2];
-    }, 4096);
-  }
-  for (int64_t i = 0; i < d->te_off[n_te]; ++i) col_te[d->te_songs[i]]++;
-  {
-    const int64_t s_bad = first_bad(n_s, [&](int64_t s2) {
-      return d->song_count[s2] < col_tr[s2] + col_te[s2] || d->song_count[s2] <= 0;
-    });
-    if (s_bad >= 0)
-      return fail(MR_E_INVALID, "song %d: count %d below its %d distinct listeners (or zero)", (int)s_bad,
-                  d->song_count[s_bad], col_tr[s_bad] + col_te[s_bad]);
-  }
   std::vector<int64_t> trs_off((size_t)n_s + 1, 0);
   for (int s2 = 0; s2 < n_s; ++s2) trs_off[s2 + 1] = trs_off[s2] + col_tr[s2];
   trace("counts");
@@ -2538,8 +2560,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     const size_t nc = (size_t)(wide ? batch : n_te) * n_tiles * k;
     if ((rc = dev_alloc(c->cand_key, nc))) return rc;
     if ((rc = dev_alloc(c->cand_song, nc))) return rc;
-    if ((rc = dev_alloc(c->top_key, (size_t)n_te * k))) return rc;
-    if ((rc = dev_alloc(c->top_song, (size_t)n_te * k))) return rc;
+    // keys then songs in ONE record block: the send buffer of the song-shard
+    // exchange (one all-gather of rec bytes per shard, mr_topk_merge_records_async)
+    const size_t nk = (size_t)n_te * k;
+    if ((rc = dev_alloc(c->top_key, (size_t)topk_record_bytes(nk) / 8))) return rc;
+    c->top_song.p = reinterpret_cast<int*>(c->top_key.p + nk);
+    c->top_song.n = nk;
+    c->top_song.own = false;
     if ((rc = dev_alloc(c->top_score, (size_t)n_te * k))) return rc;
     if ((rc = dev_alloc(c->counter, (size_t)n_te))) return rc;
     MR_HIP(hipMemsetAsync(c->counter.p, 0, (size_t)n_te * sizeof(unsigned), st));
@@ -2715,7 +2742,7 @@ int run_model(mr_ctx* c, int model) {
                          c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
       if (wide && k > 0 && c->n_tiles > 1) {  // per-user top-k over the tiles' candidates
-        MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, c->cand_key.p, c->cand_song.p,
+        MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, (long long)k, c->cand_key.p, c->cand_song.p,
                        c->top_key.p + (size_t)(user0 + y0) * k, c->top_song.p + (size_t)(user0 + y0) * k,
                        c->top_score.p + (size_t)(user0 + y0) * k};
         hipLaunchKernelGGL(k_topk_merge, dim3(ny), dim3(kThreads), c->merge_lds, st, mp);
@@ -2732,13 +2759,8 @@ int run_model(mr_ctx* c, int model) {
 
 namespace mr_internal {
 
-int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
-                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
-  if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
-  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
-  MR_HIP(hipSetDevice(c->opt.device));
-  MergeParams mp{n_shards, k, k, k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in), songs_in,
-                 reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
+namespace {
+int launch_merge(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const MergeParams& mp) {
   const int lds = merge_lds_bytes(k);
   if (lds > 160 * 1024) return fail(MR_E_INVALID, "merge of %d lists x %d needs too much LDS", n_shards, k);
   MR_HIP(hipFuncSetAttribute((const void*)k_topk_merge, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -2754,8 +2776,49 @@ int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int3
   MR_HIP(hipGetLastError());
   return MR_OK;
 }
+}  // namespace
+
+int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
+                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
+  if (!c || !songs_in || !keys_in || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
+  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
+  MR_HIP(hipSetDevice(c->opt.device));
+  MergeParams mp{n_shards, k, k, k, (long long)n_te * k, (long long)n_te * k, reinterpret_cast<const long long*>(keys_in),
+                 songs_in, reinterpret_cast<long long*>(keys_out), songs_out, scores_out};
+  return launch_merge(c, n_shards, n_te, k, mp);
+}
+
+int merge_records_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const void* records, int64_t rec_bytes,
+                        int32_t* songs_out, int64_t* keys_out, double* scores_out) {
+  if (!c || !records || !songs_out || !keys_out) return fail(MR_E_INVALID, "null argument");
+  if (n_shards <= 0 || n_te <= 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad merge shape");
+  const size_t nk = (size_t)n_te * k;
+  if (rec_bytes < (int64_t)(12 * nk) || rec_bytes % 8)
+    return fail(MR_E_INVALID, "record blocks of %lld B cannot hold %zu keys + songs (multiple of 8 B needed)",
+                (long long)rec_bytes, nk);
+  MR_HIP(hipSetDevice(c->opt.device));
+  const char* base = static_cast<const char*>(records);
+  MergeParams mp{n_shards, k, k, k, rec_bytes / 8, rec_bytes / 4, reinterpret_cast<const long long*>(base),
+                 reinterpret_cast<const int*>(base + 8 * nk), reinterpret_cast<long long*>(keys_out), songs_out,
+                 scores_out};
+  return launch_merge(c, n_shards, n_te, k, mp);
+}
+
+int topk_records(mr_ctx* c, void** records, int64_t* rec_bytes) {
+  if (!c || !records || !rec_bytes) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded || c->opt.topk <= 0) return fail(MR_E_STATE, "no top-k lists (not loaded or topk = 0)");
+  *records = c->top_key.p;
+  *rec_bytes = topk_record_bytes((size_t)c->n_te * c->opt.topk);
+  return MR_OK;
+}
 
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+int validate_dataset(const mr_dataset* d) {
+  if (!d) return fail(MR_E_INVALID, "null dataset");
+  std::vector<int32_t> col_tr;
+  return check_dataset(d, col_tr);
+}
 
 }  // namespace mr_internal
 
@@ -2876,6 +2939,17 @@ int mr_copy_topk_device_async(mr_ctx* c, int32_t* songs, int64_t* keys) {
 int mr_topk_merge_device_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
                                const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
   return mr_internal::merge_async(c, n_shards, n_te, k, songs_in, keys_in, songs_out, keys_out, scores_out);
+}
+
+int mr_topk_record_bytes(int32_t n_te, int32_t k, int64_t* rec_bytes) {
+  if (!rec_bytes || n_te < 0 || k <= 0 || k > kMaxTopK) return fail(MR_E_INVALID, "bad record shape");
+  *rec_bytes = topk_record_bytes((size_t)n_te * k);
+  return MR_OK;
+}
+
+int mr_topk_merge_records_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const void* records,
+                                int64_t rec_bytes, int32_t* songs_out, int64_t* keys_out, double* scores_out) {
+  return mr_internal::merge_records_async(c, n_shards, n_te, k, records, rec_bytes, songs_out, keys_out, scores_out);
 }
 
 int mr_score_dense(mr_ctx* c, int model, void* out) {

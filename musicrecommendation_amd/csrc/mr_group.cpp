@@ -30,6 +30,9 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -73,17 +76,27 @@ struct Rccl {
   decltype(&ncclGetErrorString) error_string = nullptr;
 };
 
-Rccl& rccl() {
-  static Rccl r;
+// The library: MR_RCCL_LIB when set (tests/fake_rccl runs the multi-context
+// path on one GPU), else librccl. One handle per path, loaded once.
+Rccl& rccl_at(const std::string& path) {
+  static std::mutex mu;
+  static std::map<std::string, Rccl> libs;
+  std::lock_guard<std::mutex> lock(mu);
+  Rccl& r = libs[path];
   if (r.tried) return r;
   r.tried = true;
   void* h = nullptr;
-  for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
-    h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
-    if (h) break;
+  if (!path.empty()) {
+    h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  } else {
+    for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+      h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (h) break;
+    }
   }
   if (!h) {
-    r.why = std::string("dlopen(librccl.so.1): ") + dlerror();
+    const char* e = dlerror();
+    r.why = std::string("dlopen(") + (path.empty() ? "librccl.so.1" : path) + "): " + (e ? e : "?");
     return r;
   }
   r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
@@ -93,15 +106,20 @@ Rccl& rccl() {
   r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
   r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.group_start && r.group_end && r.error_string;
-  if (!r.ok) r.why = "librccl lacks a required symbol";
+  if (!r.ok) r.why = "the RCCL library lacks a required symbol";
   return r;
+}
+
+std::string rccl_path() {
+  const char* e = std::getenv("MR_RCCL_LIB");
+  return e ? std::string(e) : std::string();
 }
 
 #define G_NCCL(call)                                                                             \
   do {                                                                                           \
     ncclResult_t r_ = (call);                                                                    \
     if (r_ != ncclSuccess)                                                                       \
-      return gfail(MR_E_RCCL, "%s failed: %s (%s:%d)", #call, rccl().error_string(r_), __FILE__, \
+      return gfail(MR_E_RCCL, "%s failed: %s (%s:%d)", #call, G->rc->error_string(r_), __FILE__, \
                    __LINE__);                                                                    \
   } while (0)
 
@@ -135,8 +153,10 @@ struct Member {
   hipStream_t stream = nullptr;  // the context's own stream
   hipEvent_t done = nullptr;     // end of this member's part of the last run / exchange
   ncclComm_t comm = nullptr;     // RCCL: communicator of the member's user block
-  Buf<long long> gkey, mkey;     // gathered [G_s][n_bk][k] / merged [n_bk][k] lists
-  Buf<int> gsong, msong;
+  Buf<unsigned char> grec;       // gathered top-k record blocks [G_s][rec] (keys, then songs)
+  int64_t rec = 0;               // bytes of one record block of this member's user block
+  Buf<long long> mkey;           // merged [n_bk][k] lists
+  Buf<int> msong;
   Buf<double> mscore;
   Buf<unsigned char> send, recv;  // RCCL dense: [n_bk][w_max] own shard, [G_s][n_bk][w_max] gathered
 };
@@ -151,6 +171,7 @@ struct mr_group {
   bool loaded = false, ran = false;
   std::vector<Member> m;  // index b * G_s + g
   std::vector<int> dev_of;
+  Rccl* rc = nullptr;     // the RCCL library of this group (RCCL transport)
 
   int gs() const { return gopt.n_song_shards; }
   int gu() const { return gopt.n_user_blocks; }
@@ -166,9 +187,9 @@ struct mr_group {
       }
     }
     for (auto& x : m) {
-      x.gkey.release(); x.mkey.release(); x.gsong.release(); x.msong.release(); x.mscore.release();
+      x.grec.release(); x.mkey.release(); x.msong.release(); x.mscore.release();
       x.send.release(); x.recv.release();
-      if (x.comm) (void)rccl().comm_destroy(x.comm);
+      if (x.comm && rc) (void)rc->comm_destroy(x.comm);
       x.comm = nullptr;
       if (x.done) { (void)hipSetDevice(x.dev); (void)hipEventDestroy(x.done); }
       x.done = nullptr;
@@ -243,20 +264,20 @@ int run_group(mr_group* G, int model) {
   if (!G->exchange()) return MR_OK;
   const int gs = G->gs();
   if (rc_mode) {
-    Rccl& R = rccl();
+    Rccl& R = *G->rc;
     G_NCCL(R.group_start());
-    // Every call between ncclGroupStart and ncclGroupEnd; an error still
-    // closes the group (RCCL's group state is thread-global).
+    // ONE all-gather per member: its top-k record block (keys, then songs;
+    // n_bk x k x 12 B) into [G_s][rec]. Every call between ncclGroupStart and
+    // ncclGroupEnd; an error still closes the group (thread-global state).
     auto enqueue = [&]() -> int {
       for (auto& x : G->m) {
-        const size_t n = (size_t)(x.user_hi - x.user_lo) * k;
-        int32_t* ts;
-        int64_t* tk;
-        int rc = mr_device_outputs(x.ctx, nullptr, &ts, &tk, nullptr);
+        void* rec;
+        int64_t bytes;
+        int rc = mr_internal::topk_records(x.ctx, &rec, &bytes);
         if (rc) return rc;
+        if (bytes != x.rec) return gfail(MR_E_STATE, "record block of %lld B, %lld expected", (long long)bytes, (long long)x.rec);
         G_HIP(hipSetDevice(x.dev));
-        G_NCCL(R.all_gather(tk, x.gkey.p, n, ncclInt64, x.comm, x.stream));
-        G_NCCL(R.all_gather(ts, x.gsong.p, n, ncclInt32, x.comm, x.stream));
+        G_NCCL(R.all_gather(rec, x.grec.p, (size_t)bytes / 8, ncclInt64, x.comm, x.stream));
       }
       return MR_OK;
     };
@@ -265,33 +286,29 @@ int run_group(mr_group* G, int model) {
     if (erc) return erc;
     if (end != ncclSuccess) return gfail(MR_E_RCCL, "ncclGroupEnd: %s", R.error_string(end));
     for (auto& x : G->m) {
-      const int rc = mr_internal::merge_async(x.ctx, gs, x.user_hi - x.user_lo, k, x.gsong.p,
-                                              reinterpret_cast<const int64_t*>(x.gkey.p), x.msong.p,
-                                              reinterpret_cast<int64_t*>(x.mkey.p), x.mscore.p);
+      const int rc = mr_internal::merge_records_async(x.ctx, gs, x.user_hi - x.user_lo, k, x.grec.p, x.rec, x.msong.p,
+                                                      reinterpret_cast<int64_t*>(x.mkey.p), x.mscore.p);
       if (rc) return rc;
     }
     return MR_OK;
   }
-  for (int b = 0; b < G->gu(); ++b) {  // COPY: the block root gathers and merges
+  for (int b = 0; b < G->gu(); ++b) {  // COPY: the block root gathers the record blocks and merges
     Member& r = G->at(b, 0);
-    const size_t n = (size_t)(r.user_hi - r.user_lo) * k;
     for (int g = 0; g < gs; ++g) {
       Member& x = G->at(b, g);
       if (g > 0) {
         int rc = wait_member(r, x);
         if (rc) return rc;
       }
-      int32_t* ts;
-      int64_t* tk;
-      int rc = mr_device_outputs(x.ctx, nullptr, &ts, &tk, nullptr);
+      void* rec;
+      int64_t bytes;
+      int rc = mr_internal::topk_records(x.ctx, &rec, &bytes);
       if (rc) return rc;
       G_HIP(hipSetDevice(r.dev));
-      G_HIP(hipMemcpyAsync(r.gkey.p + (size_t)g * n, tk, n * 8, hipMemcpyDeviceToDevice, r.stream));
-      G_HIP(hipMemcpyAsync(r.gsong.p + (size_t)g * n, ts, n * 4, hipMemcpyDeviceToDevice, r.stream));
+      G_HIP(hipMemcpyAsync(r.grec.p + (size_t)g * r.rec, rec, (size_t)bytes, hipMemcpyDeviceToDevice, r.stream));
     }
-    const int rc = mr_internal::merge_async(r.ctx, gs, r.user_hi - r.user_lo, k, r.gsong.p,
-                                            reinterpret_cast<const int64_t*>(r.gkey.p), r.msong.p,
-                                            reinterpret_cast<int64_t*>(r.mkey.p), r.mscore.p);
+    const int rc = mr_internal::merge_records_async(r.ctx, gs, r.user_hi - r.user_lo, k, r.grec.p, r.rec, r.msong.p,
+                                                    reinterpret_cast<int64_t*>(r.mkey.p), r.mscore.p);
     if (rc) return rc;
   }
   return MR_OK;
@@ -375,15 +392,23 @@ int mr_group_create(const mr_options* opt, const mr_group_options* gopt, mr_grou
   if (transport == MR_TRANSPORT_AUTO) transport = n_distinct > 1 ? MR_TRANSPORT_RCCL : MR_TRANSPORT_COPY;
   if (transport == MR_TRANSPORT_COPY && n_distinct > 1)
     return gfail(MR_E_INVALID, "COPY transport keeps every context on one device (%d devices given)", n_distinct);
-  if (transport == MR_TRANSPORT_RCCL && n_distinct != G)
+  // RCCL needs one distinct device per context; only a library named by
+  // MR_RCCL_LIB (tests/fake_rccl: the multi-context path on one GPU) may be
+  // handed shared devices — real RCCL is never asked for two ranks on one GPU.
+  if (transport == MR_TRANSPORT_RCCL && n_distinct != G && rccl_path().empty())
     return gfail(MR_E_INVALID, "RCCL transport needs one distinct device per context (%d contexts, %d devices)", G,
                  n_distinct);
-  if (transport == MR_TRANSPORT_RCCL && !rccl().ok) return gfail(MR_E_RCCL, "RCCL unavailable: %s", rccl().why.c_str());
+  Rccl* R = nullptr;
+  if (transport == MR_TRANSPORT_RCCL) {
+    R = &rccl_at(rccl_path());
+    if (!R->ok) return gfail(MR_E_RCCL, "RCCL unavailable: %s", R->why.c_str());
+  }
   mr_group* g = new mr_group();
   g->opt = o;
   g->gopt = go;
   g->gopt.devices = nullptr;  // not retained
   g->transport = transport;
+  g->rc = R;
   g->dev_of = dev;
   g->m.resize(G);
   for (int i = 0; i < G; ++i) {
@@ -412,11 +437,11 @@ int mr_group_create(const mr_options* opt, const mr_group_options* gopt, mr_grou
       std::vector<ncclComm_t> comms(go.n_song_shards);
       std::vector<int> devs(go.n_song_shards);
       for (int s = 0; s < go.n_song_shards; ++s) devs[s] = g->at(b, s).dev;
-      const ncclResult_t r = rccl().comm_init_all(comms.data(), go.n_song_shards, devs.data());
+      const ncclResult_t r = R->comm_init_all(comms.data(), go.n_song_shards, devs.data());
       if (r != ncclSuccess) {
         g->release_members();
         delete g;
-        return gfail(MR_E_RCCL, "ncclCommInitAll over %d devices: %s", go.n_song_shards, rccl().error_string(r));
+        return gfail(MR_E_RCCL, "ncclCommInitAll over %d devices: %s", go.n_song_shards, R->error_string(r));
       }
       for (int s = 0; s < go.n_song_shards; ++s) g->at(b, s).comm = comms[s];
     }
@@ -434,12 +459,22 @@ int mr_group_destroy(mr_group* g) {
 
 int mr_group_load(mr_group* g, const mr_dataset* d) {
   if (!g || !d) return gfail(MR_E_INVALID, "null argument");
-  if (d->n_test_users < g->gu() || d->n_songs < g->gs() || !d->te_off || !d->tr_off || !d->te_len)
+  // mr_load's checks first: song_bounds below indexes by the caller's song ids
+  if (int rc = mr_internal::validate_dataset(d)) return rc;
+  if (d->n_test_users < g->gu() || d->n_songs < g->gs())
     return gfail(MR_E_INVALID, "%d test users / %d songs cannot form %d user blocks x %d song shards",
                  d->n_test_users, d->n_songs, g->gu(), g->gs());
   int rc = sync_all(g);
   if (rc) return rc;
   g->loaded = g->ran = false;
+  // A reload frees the old contexts' device data before the new ones load
+  // (else device memory peaks at two full loads). The contexts themselves are
+  // recreated below: the shard geometry is a creation option.
+  for (auto& x : g->m) {
+    if (x.ctx) mr_destroy(x.ctx);
+    x.ctx = nullptr;
+    x.stream = nullptr;
+  }
   int tile = 0;  // the wide shape's tile when the contexts will use it (mr_shard_tile_songs)
   if (int rc = mr_shard_tile_songs(&g->opt, d->n_train_users, d->n_test_users / g->gu(), &tile)) return rc;
   const std::vector<int> sb = song_bounds(d, g->gs(), tile);
@@ -485,7 +520,6 @@ int mr_group_load(mr_group* g, const mr_dataset* d) {
           rcs[i] = r;
           return;
         }
-        mr_destroy(x.ctx);
         x.ctx = c;
         x.stream = (hipStream_t)mr_stream(c);
       });
@@ -499,9 +533,11 @@ int mr_group_load(mr_group* g, const mr_dataset* d) {
   for (auto& x : g->m) {
     const size_t n = (size_t)(x.user_hi - x.user_lo) * std::max(k, 1);
     const bool holds = rc_mode || x.shard == 0;  // gathers + merges here
+    x.rec = 0;
+    if (k > 0 && (rc = mr_topk_record_bytes(x.user_hi - x.user_lo, k, &x.rec))) return rc;
     if (g->exchange() && holds) {
-      if ((rc = alloc(x.gkey, x.dev, n * g->gs())) || (rc = alloc(x.gsong, x.dev, n * g->gs())) ||
-          (rc = alloc(x.mkey, x.dev, n)) || (rc = alloc(x.msong, x.dev, n)) || (rc = alloc(x.mscore, x.dev, n)))
+      if ((rc = alloc(x.grec, x.dev, (size_t)x.rec * g->gs())) || (rc = alloc(x.mkey, x.dev, n)) ||
+          (rc = alloc(x.msong, x.dev, n)) || (rc = alloc(x.mscore, x.dev, n)))
         return rc;
     }
     if (rc_mode && g->opt.dense)
@@ -629,6 +665,7 @@ int mr_group_score_dense(mr_group* g, int model, void* out) {
 }
 
 int mr_group_allgather_dense(mr_group* g, void* const* dst) {
+  mr_group* G = g;  // G_NCCL reports through G->rc
   if (!g || !dst) return gfail(MR_E_INVALID, "null argument");
   if (!g->ran) return gfail(MR_E_STATE, "no mr_group_run yet");
   if (!g->opt.dense) return gfail(MR_E_STATE, "group created with dense=0");
@@ -641,7 +678,7 @@ int mr_group_allgather_dense(mr_group* g, void* const* dst) {
         if (rc) return rc;
       }
     }
-    Rccl& R = rccl();
+    Rccl& R = *g->rc;
     const ncclDataType_t t = g->opt.out_dtype == MR_OUT_F64 ? ncclFloat64 : ncclFloat32;
     G_NCCL(R.group_start());
     auto enqueue = [&]() -> int {

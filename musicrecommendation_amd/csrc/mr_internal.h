@@ -14,6 +14,19 @@ namespace mr_internal {
 int merge_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const int32_t* songs_in,
                 const int64_t* keys_in, int32_t* songs_out, int64_t* keys_out, double* scores_out);
 
+// The same over G gathered record blocks (keys [n_te*k] int64 at byte 0,
+// songs [n_te*k] int32 at byte 8*n_te*k, block stride rec_bytes).
+int merge_records_async(mr_ctx* c, int32_t n_shards, int32_t n_te, int32_t k, const void* records, int64_t rec_bytes,
+                        int32_t* songs_out, int64_t* keys_out, double* scores_out);
+
+// The context's own top-k record block (the exchange's send buffer; valid
+// until mr_load / mr_destroy) and its size in bytes.
+int topk_records(mr_ctx* c, void** records, int64_t* rec_bytes);
+
+// mr_load's input checks (CSR shapes, sorted rows, id ranges, counts) without
+// loading: what mr_group_load runs before it reads the dataset itself.
+int validate_dataset(const mr_dataset* d);
+
 // Set the calling thread's mr_last_error() message; returns code.
 int set_error(int code, const char* msg);
 

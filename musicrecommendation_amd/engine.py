@@ -155,6 +155,27 @@ class Engine:
                                                     keys_ptr, out_songs_ptr, out_keys_ptr, out_scores_ptr or None)
         _lib.check(rc, "mr_topk_merge_device")
 
+    def record_bytes(self) -> int:
+        """Bytes of this engine's top-k record block (keys then songs, padded):
+        the unit of the single all-gather of a song-sharded exchange."""
+        b = ctypes.c_int64()
+        _lib.check(self._L.mr_topk_record_bytes(self.n_test, self.topk_k, ctypes.byref(b)), "mr_topk_record_bytes")
+        return b.value
+
+    def copy_topk_record(self, record_ptr: int, wait: bool = False) -> None:
+        """Copy the last run's lists into a device record block (keys at byte 0,
+        songs at byte 8 * n_test * k)."""
+        n = self.n_test * self.topk_k
+        self.copy_topk_device(record_ptr + 8 * n, record_ptr, wait=wait)
+
+    def merge_topk_records(self, n_shards: int, records_ptr: int, rec_bytes: int, out_songs_ptr: int,
+                           out_keys_ptr: int, out_scores_ptr: int = 0) -> None:
+        """Merge n_shards gathered record blocks (stride rec_bytes) on this GPU,
+        enqueued on the engine stream."""
+        _lib.check(self._L.mr_topk_merge_records_async(self._h, n_shards, self.n_test, self.topk_k, records_ptr,
+                                                       rec_bytes, out_songs_ptr, out_keys_ptr, out_scores_ptr or None),
+                   "mr_topk_merge_records_async")
+
     # ---- device-resident models (combination models, evaluation) -------------
     def run_into(self, model: Union[str, int], dense_ptr: int) -> None:
         """Asynchronous: like run(), the dense model written to a caller-owned

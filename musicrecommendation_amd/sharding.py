@@ -7,9 +7,9 @@ layout inside the C ABI for single-process callers):
 * song-range shards (the north star; the reference's Spark "strategy 2",
   distributed.scala:477-479 ``parallelize(songs, 4)``): every rank holds the
   whole train CSR (stage 1 is replicated) and scores songs [lo, hi). Dense
-  rows stay sharded by column; the per-test-user top-k lists are exchanged
-  with ONE all-gather of (int64 key, int32 song) and merged by
-  (key desc, song asc). Fixed-point keys make the merge order-independent,
+  rows stay sharded by column; the per-test-user top-k lists travel as one
+  record block per rank (int64 keys, then int32 songs) exchanged with ONE
+  all-gather and merged by (key desc, song asc). Fixed-point keys make the merge order-independent,
   so the result is bit-identical for any shard count.
 * test-user blocks (Spark "strategy 1", distributed.scala:468-470): each rank
   scores its own test users over all songs; no exchange at all. This is the
@@ -82,28 +82,50 @@ def user_blocks(n_test: int, n_blocks: int) -> List[Tuple[int, int]]:
     return [(n_test * b // n_blocks, n_test * (b + 1) // n_blocks) for b in range(n_blocks)]
 
 
+def pack_records(songs, keys):
+    """One rank's lists as a record block (torch uint8): n int64 keys, then n
+    int32 songs, padded to 16 B — the layout of mr_topk_record_bytes."""
+    import torch
+
+    n = songs.numel()
+    rec = -(-12 * n // 16) * 16
+    out = torch.zeros(rec, dtype=torch.uint8, device=songs.device)
+    out[:8 * n] = keys.contiguous().reshape(-1).view(torch.uint8)
+    out[8 * n:12 * n] = songs.contiguous().reshape(-1).view(torch.uint8)
+    return out
+
+
+def unpack_records(g_rec, world: int, n_te: int, k: int):
+    """[world][rec] gathered blocks -> (songs [world, n_te, k], keys [world, n_te, k])."""
+    import torch
+
+    n = n_te * k
+    blocks = g_rec.view(world, -1)
+    keys = blocks[:, :8 * n].contiguous().view(torch.int64).view(world, n_te, k)
+    songs = blocks[:, 8 * n:12 * n].contiguous().view(torch.int32).view(world, n_te, k)
+    return songs, keys
+
+
 def exchange_topk(songs, keys, group=None):
     """All-gather per-rank top-k lists (torch tensors [n_test, k], int32 songs,
-    int64 keys, song ids global) and merge them by (key desc, song asc).
-
-    CUDA tensors: RCCL all-gather over xGMI + the engine's merge kernel (the
-    caller passes ``engine``-backed merge via ``merge_device``). CPU tensors
-    (gloo): the same all-gather + the engine library's host merge. Returns
-    merged (songs, keys) tensors on the input device.
-    """
-    import torch
+    int64 keys, song ids global) as ONE collective over packed record blocks
+    (pack_records); returns the gathered (songs, keys), each
+    [world, n_test, k], on the input device, ready for a merge by (key desc,
+    song asc) (merge_gathered_host, or the engine's record merge on a GPU).
+    CUDA tensors under a gloo group are gathered on the host (rehearsals)."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     n_te, k = songs.shape
-    g_songs = torch.empty((world * n_te, k), dtype=songs.dtype, device=songs.device)
-    g_keys = torch.empty((world * n_te, k), dtype=keys.dtype, device=keys.device)
     if songs.is_cuda and dist.get_backend(group) != "nccl":  # gloo rehearsal: gather on the host
         gs, gk = exchange_topk(songs.cpu(), keys.cpu(), group)
         return gs.to(songs.device), gk.to(keys.device)
-    dist.all_gather_into_tensor(g_songs, songs.contiguous(), group=group)
-    dist.all_gather_into_tensor(g_keys, keys.contiguous(), group=group)
-    return g_songs.view(world, n_te, k), g_keys.view(world, n_te, k)
+    rec = pack_records(songs, keys)
+    import torch
+
+    g_rec = torch.empty(world * rec.numel(), dtype=torch.uint8, device=rec.device)
+    dist.all_gather_into_tensor(g_rec, rec, group=group)
+    return unpack_records(g_rec, world, n_te, k)
 
 
 def merge_gathered_host(g_songs, g_keys):
@@ -174,13 +196,14 @@ class ShardScorer:
                              block_songs=block_songs)
         self.device = torch.device("cuda", device)
         n_te = self.ds.n_test
-        self.local_songs = torch.empty((n_te, topk), dtype=torch.int32, device=self.device)
-        self.local_keys = torch.empty((n_te, topk), dtype=torch.int64, device=self.device)
+        # the exchange: this rank's lists as ONE record block (keys, then songs),
+        # all-gathered in one collective into [G_s][rec] and merged on the device
+        self.rec_bytes = self.engine.record_bytes()
+        self.local_rec = torch.empty(self.rec_bytes // 8, dtype=torch.int64, device=self.device)
+        self.g_rec = torch.empty(self.gs * (self.rec_bytes // 8), dtype=torch.int64, device=self.device)
         self.out_songs = torch.empty((n_te, topk), dtype=torch.int32, device=self.device)
         self.out_keys = torch.empty((n_te, topk), dtype=torch.int64, device=self.device)
         self.out_scores = torch.empty((n_te, topk), dtype=torch.float64, device=self.device)
-        self.g_songs = torch.empty((self.gs * n_te, topk), dtype=torch.int32, device=self.device)
-        self.g_keys = torch.empty((self.gs * n_te, topk), dtype=torch.int64, device=self.device)
         self._ext = torch.cuda.ExternalStream(self.engine.stream, device=self.device)
 
     def pairs(self) -> int:
@@ -192,26 +215,31 @@ class ShardScorer:
     def step(self, model: str) -> None:
         """Score the (block, shard) cell, then exchange + merge the block's top-k
         lists. Asynchronous: returns with the work queued on the streams."""
+        self.engine.run(model)
+        if self.gs > 1:
+            self.exchange()
+
+    def exchange(self) -> None:
+        """The exchange step alone (after a run): this rank's record block
+        copied out, ONE all-gather inside the block's group, the merge on the
+        device. Asynchronous; the engine stream and torch's stream are ordered
+        with events."""
         import torch
         import torch.distributed as dist
 
         e = self.engine
-        e.run(model)
-        if self.gs == 1:
-            return
-        e.copy_topk_device(self.local_songs.data_ptr(), self.local_keys.data_ptr(), wait=False)
+        e.copy_topk_record(self.local_rec.data_ptr())
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(self._ext)  # lists copied before the all-gather reads them
         if dist.get_backend(self.group) == "nccl":
-            dist.all_gather_into_tensor(self.g_songs, self.local_songs, group=self.group)
-            dist.all_gather_into_tensor(self.g_keys, self.local_keys, group=self.group)
+            dist.all_gather_into_tensor(self.g_rec, self.local_rec, group=self.group)
         else:  # gloo rehearsal with CUDA tensors: gather on the host
-            gs_, gk_ = exchange_topk(self.local_songs.cpu(), self.local_keys.cpu(), self.group)
-            self.g_songs.copy_(gs_.reshape(self.g_songs.shape))
-            self.g_keys.copy_(gk_.reshape(self.g_keys.shape))
-        self._ext.wait_stream(cur)  # the merge reads the gathered lists
-        e.merge_topk_device(self.gs, self.g_songs.data_ptr(), self.g_keys.data_ptr(), self.out_songs.data_ptr(),
-                            self.out_keys.data_ptr(), self.out_scores.data_ptr(), wait=False)
+            parts = [torch.empty_like(self.local_rec, device="cpu") for _ in range(self.gs)]
+            dist.all_gather(parts, self.local_rec.cpu(), group=self.group)
+            self.g_rec.copy_(torch.cat(parts))
+        self._ext.wait_stream(cur)  # the merge reads the gathered blocks
+        e.merge_topk_records(self.gs, self.g_rec.data_ptr(), self.rec_bytes, self.out_songs.data_ptr(),
+                             self.out_keys.data_ptr(), self.out_scores.data_ptr())
 
     def sync(self) -> None:
         import torch

@@ -33,6 +33,17 @@ case ",$STEPS," in *,prof,*)
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 200 ;;
 esac
+case ",$STEPS," in *,c4,*) run bench_c4 900 python -u bench.py --config c4 --steps 5 --warmup 2 ;; esac
+case ",$STEPS," in *,c5,*) run bench_c5 900 python -u bench.py --config c5 --steps 3 --warmup 1 ;; esac
+# Rehearsal of the driver's N>1 command on one GPU (gloo, every rank on device 0;
+# the real runs use RCCL, one GPU per rank): the C2 line + its north_star block.
+for n in 2 4; do
+  case ",$STEPS," in *,rehearse$n,*)
+    MR_BENCH_BACKEND=gloo MR_BENCH_DEVICE=0 PYTHONUNBUFFERED=1 run rehearse_n$n 900 python -m torch.distributed.run \
+      --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n \
+      --steps 50 --warmup 5 --no-cpu-baseline ;;
+  esac
+done
 case ",$STEPS," in *,c3,*) run bench_c3 600 python bench.py --config c3 --no-cpu-baseline --steps 20 --warmup 3 ;; esac
 case ",$STEPS," in *,profc3,*)
   export TMPDIR=/tmp

@@ -1,0 +1,154 @@
+// fake_rccl.cpp — TEST INFRASTRUCTURE: the five RCCL entry points the engine's
+// group (musicrecommendation_amd/csrc/mr_group.cpp) loads, implemented with
+// HIP device copies, so its multi-context RCCL path runs on a one-GPU box
+// (real RCCL refuses two ranks on one device). Selected with
+// MR_RCCL_LIB=<path to libfake_rccl.so>; never used by the product.
+//
+// Semantics kept from RCCL: ncclCommInitAll creates one communicator per
+// entry of the device list (duplicates allowed here); ncclAllGather of rank r
+// places r's send block at recv + r * bytes on every rank; calls made by one
+// thread for several ranks must sit between ncclGroupStart / ncclGroupEnd, and
+// the collective is stream-ordered on every rank's stream: no copy starts
+// before every rank's stream reached the call, and no rank's stream passes it
+// before every copy that reads its send buffer is done.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <memory>
+#include <vector>
+
+struct Clique {
+  std::vector<int> dev;
+};
+
+struct ncclComm {
+  std::shared_ptr<Clique> clique;
+  int rank = 0;
+};
+
+namespace {
+
+struct Op {
+  const void* send;
+  void* recv;
+  size_t bytes;
+  ncclComm_t comm;
+  hipStream_t stream;
+};
+
+thread_local int g_depth = 0;
+thread_local std::vector<Op> g_ops;
+
+size_t type_size(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return 0;
+  }
+}
+
+// One collective over a whole clique: ops[r] is rank r's call.
+ncclResult_t run_allgather(const std::vector<Op*>& ops) {
+  const size_t n = ops.size(), bytes = ops[0]->bytes;
+  std::vector<hipEvent_t> arrive(n), leave(n);
+  for (size_t r = 0; r < n; ++r) {
+    const int dev = ops[r]->comm->clique->dev[r];
+    if (hipSetDevice(dev) != hipSuccess || hipEventCreateWithFlags(&arrive[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&leave[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(arrive[r], ops[r]->stream) != hipSuccess)
+      return ncclUnhandledCudaError;
+  }
+  for (size_t r = 0; r < n; ++r) {
+    (void)hipSetDevice(ops[r]->comm->clique->dev[r]);
+    for (size_t p = 0; p < n; ++p)
+      if (hipStreamWaitEvent(ops[r]->stream, arrive[p], 0) != hipSuccess) return ncclUnhandledCudaError;
+    for (size_t p = 0; p < n; ++p)
+      if (hipMemcpyAsync(static_cast<char*>(ops[r]->recv) + p * bytes, ops[p]->send, bytes, hipMemcpyDeviceToDevice,
+                         ops[r]->stream) != hipSuccess)
+        return ncclUnhandledCudaError;
+    if (hipEventRecord(leave[r], ops[r]->stream) != hipSuccess) return ncclUnhandledCudaError;
+  }
+  for (size_t r = 0; r < n; ++r) {
+    (void)hipSetDevice(ops[r]->comm->clique->dev[r]);
+    for (size_t p = 0; p < n; ++p)
+      if (hipStreamWaitEvent(ops[r]->stream, leave[p], 0) != hipSuccess) return ncclUnhandledCudaError;
+  }
+  for (size_t r = 0; r < n; ++r) {  // destroyed once the recorded work completes
+    (void)hipEventDestroy(arrive[r]);
+    (void)hipEventDestroy(leave[r]);
+  }
+  return ncclSuccess;
+}
+
+ncclResult_t flush() {
+  std::vector<Op> ops;
+  ops.swap(g_ops);
+  std::map<Clique*, std::vector<Op*>> by;
+  for (Op& o : ops) {
+    auto& v = by[o.comm->clique.get()];
+    if (v.empty()) v.assign(o.comm->clique->dev.size(), nullptr);
+    if (v[o.comm->rank]) return ncclInvalidUsage;  // two calls of one rank in one group
+    v[o.comm->rank] = &o;
+  }
+  for (auto& kv : by) {
+    for (Op* o : kv.second)
+      if (!o || o->bytes != kv.second[0]->bytes) return ncclInvalidUsage;  // a rank missing / sizes differ
+    const ncclResult_t r = run_allgather(kv.second);
+    if (r != ncclSuccess) return r;
+  }
+  return ncclSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+ncclResult_t ncclCommInitAll(ncclComm_t* comm, int ndev, const int* devlist) {
+  if (!comm || ndev < 1) return ncclInvalidArgument;
+  auto c = std::make_shared<Clique>();
+  for (int i = 0; i < ndev; ++i) c->dev.push_back(devlist ? devlist[i] : i);
+  for (int i = 0; i < ndev; ++i) {
+    comm[i] = new ncclComm();
+    comm[i]->clique = c;
+    comm[i]->rank = i;
+  }
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  delete comm;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGroupStart() {
+  ++g_depth;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGroupEnd() {
+  if (g_depth <= 0) return ncclInvalidUsage;
+  return --g_depth == 0 ? flush() : ncclSuccess;
+}
+
+ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                           ncclComm_t comm, hipStream_t stream) {
+  const size_t ts = type_size(datatype);
+  if (!comm || !ts || (!sendbuff && sendcount) || (!recvbuff && sendcount)) return ncclInvalidArgument;
+  g_ops.push_back(Op{sendbuff, recvbuff, sendcount * ts, comm, stream});
+  if (g_depth == 0) return flush();  // outside a group: only a 1-rank clique can complete
+  return ncclSuccess;
+}
+
+const char* ncclGetErrorString(ncclResult_t r) {
+  switch (r) {
+    case ncclSuccess: return "no error (fake RCCL)";
+    case ncclInvalidArgument: return "invalid argument (fake RCCL)";
+    case ncclInvalidUsage: return "invalid usage: every rank of a clique must join the group call (fake RCCL)";
+    default: return "HIP error (fake RCCL)";
+  }
+}
+
+}  // extern "C"

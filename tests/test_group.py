@@ -9,9 +9,14 @@ GPU (one MI355X): G = song shards x user blocks logical contexts on device 0
 (COPY transport: device-copy exchange) give top-k lists, keys and dense models
 bit-identical to one context, for ubm and ibm; the dense all-gather assembles
 full rows on every context; a 1-context RCCL group runs the real
-ncclCommInitAll / ncclAllGather / merge sequence. With >= 2 GPUs visible the
-RCCL transport takes over (not reachable on the 1-GPU box: RCCL refuses two
-ranks on one device)."""
+ncclCommInitAll / ncclAllGather / merge sequence; and the multi-context RCCL
+path (G = 2x1, 3x1, 2x2 communicators, one all-gather of packed top-k record
+blocks per context, the dense all-gather) runs on the one GPU through
+tests/fake_rccl (MR_RCCL_LIB: RCCL's collective semantics with device copies;
+real RCCL refuses two ranks on one device), bitwise against one context."""
+import ctypes
+import os
+
 import numpy as np
 import pytest
 
@@ -20,6 +25,25 @@ from musicrecommendation_amd.group import Group, song_shards_native
 from musicrecommendation_amd.sharding import shard_tile, song_shards
 
 from helpers import kat, dataset_from_lines, synth_fixture
+
+FAKE_RCCL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fake_rccl", "libfake_rccl.so")
+
+
+def test_fake_rccl_library_exports():
+    """The fake RCCL is built (by __graft_entry__.build) and exports what the
+    group loads; a 1-rank all-gather outside a group completes on the host
+    side of the API (no GPU work for zero bytes)."""
+    L = ctypes.CDLL(FAKE_RCCL)
+    for name in ("ncclCommInitAll", "ncclCommDestroy", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
+                 "ncclGetErrorString"):
+        assert getattr(L, name)
+    L.ncclGetErrorString.restype = ctypes.c_char_p
+    assert b"fake" in L.ncclGetErrorString(5)
+    comms = (ctypes.c_void_p * 2)()
+    assert L.ncclCommInitAll(comms, 2, (ctypes.c_int * 2)(0, 0)) == 0
+    assert L.ncclGroupEnd() == 5  # unbalanced group end: invalid usage
+    for c in comms:
+        assert L.ncclCommDestroy(ctypes.c_void_p(c)) == 0
 
 
 def _datasets():
@@ -230,3 +254,87 @@ def test_group_uneven_blocks_and_topk_only():
         assert np.array_equal(s, s_ref) and np.array_equal(k, k_ref)
         with pytest.raises(_lib.EngineError):
             g.dense()  # dense=0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [(2, 1), (3, 1), (2, 2)])
+@pytest.mark.parametrize("dense", [True, False])
+def test_multi_context_rccl_path_equals_one_context(layout, dense, monkeypatch):
+    """The RCCL transport with G_s > 1 communicators per block (one
+    ncclAllGather of the packed record blocks per context inside
+    ncclGroupStart/End, the merge on every context) through the fake RCCL on
+    one GPU: lists, keys, scores, the dense model and the dense all-gather
+    bitwise equal to one context, ubm and ibm, back-to-back runs."""
+    import torch
+    from musicrecommendation_amd.engine import Engine
+
+    monkeypatch.setenv("MR_RCCL_LIB", FAKE_RCCL)
+    gs, gu = layout
+    ds = synth.config("c2", n_test=24).dataset()
+    with Engine(ds, out_dtype="f32", topk=10, dense=dense) as e:
+        ref = {}
+        for model in ("ibm", "ubm"):
+            e.run(model)
+            ref[model] = (e.dense() if dense else None, *e.topk())
+    with Group(ds, song_shards=gs, user_blocks=gu, transport="rccl", out_dtype="f32", topk=10, dense=dense) as g:
+        assert g.transport == "rccl" and len(g.layout) == gs * gu
+        for _ in range(2):
+            for model in ("ibm", "ubm"):
+                g.run(model)
+                songs, scores, keys = g.topk()
+                d_ref, s_ref, sc_ref, k_ref = ref[model]
+                assert np.array_equal(songs, s_ref) and np.array_equal(keys, k_ref), (layout, model)
+                assert np.array_equal(scores, sc_ref, equal_nan=True), (layout, model)
+                for i in range(len(g.layout)):  # every context holds its block's merged lists
+                    ps, pk, _psc = g.device_topk(i)
+                    assert ps and pk
+                if dense:
+                    assert np.array_equal(g.dense(), d_ref, equal_nan=True), (layout, model)
+                    bufs = [torch.empty((uhi - ulo, ds.n_songs), dtype=torch.float32, device="cuda")
+                            for (_slo, _shi, ulo, uhi, _d) in g.layout]
+                    torch.cuda.synchronize()
+                    g.allgather_dense([b.data_ptr() for b in bufs])
+                    for (_slo, _shi, ulo, uhi, _d), b in zip(g.layout, bufs):
+                        assert np.array_equal(b.cpu().numpy(), d_ref[ulo:uhi], equal_nan=True), (layout, model)
+
+
+@pytest.mark.gpu
+def test_group_load_validates_before_sharding():
+    """mr_group_load runs mr_load's checks before it reads the dataset itself
+    (the shard balance indexes by song id): out-of-range ids, unsorted rows and
+    decreasing offsets are MR_E_INVALID, not heap writes."""
+    ds = synth_fixture("tiny")[0]
+    for mutate in ("song_range", "unsorted", "offsets"):
+        bad = synth_fixture("tiny")[0]
+        bad.tr_songs = bad.tr_songs.copy()
+        bad.tr_off = bad.tr_off.copy()
+        if mutate == "song_range":
+            bad.tr_songs[3] = ds.n_songs + 7
+        elif mutate == "unsorted":
+            bad.tr_songs[[0, 1]] = bad.tr_songs[[1, 0]]
+        else:
+            bad.tr_off[2] = bad.tr_off[1] - 1
+        with pytest.raises(_lib.EngineError) as e:
+            Group(bad, song_shards=2)
+        assert e.value.code == _lib.MR_E_INVALID, mutate
+
+
+@pytest.mark.gpu
+def test_group_reload():
+    """A second mr_group_load replaces the layout's data (old contexts freed
+    first) and the next run scores the new dataset."""
+    from musicrecommendation_amd.engine import Engine
+
+    a = synth.config("c2", n_test=12).dataset()
+    b = synth_fixture("small")[0]
+    with Group(a, song_shards=2, topk=10, dense=False) as g:
+        g.run("ibm")
+        cd = b.c_struct()
+        _lib.check(g._L.mr_group_load(g._h, ctypes.byref(cd)), "mr_group_load")
+        g.dataset = b
+        g.run("ibm")
+        songs, _sc, keys = g.topk()
+    with Engine(b, topk=10, dense=False) as e:
+        e.run("ibm")
+        s_ref, _sc, k_ref = e.topk()
+    assert np.array_equal(songs, s_ref) and np.array_equal(keys, k_ref)
