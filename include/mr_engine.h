@@ -377,6 +377,10 @@ int mr_group_load(mr_group* g, const mr_dataset* d);
 int mr_group_info(const mr_group* g, int32_t i, int32_t* song_lo, int32_t* song_hi, int32_t* user_lo,
                   int32_t* user_hi, int32_t* device);
 int mr_group_transport(const mr_group* g, int32_t* transport);
+/* Shape of a loaded group: contexts, test users and songs of the whole model
+ * (the sizes of mr_group_copy_dense's n_test x n_songs and of the n_test x k
+ * top-k outputs; the JNI shim checks Java array lengths against them). */
+int mr_group_shape(const mr_group* g, int32_t* n_contexts, int32_t* n_test, int32_t* n_songs);
 /* Borrowed context i (e.g. for mr_timing_begin/end on its stream); NULL on error. */
 mr_ctx* mr_group_context(mr_group* g, int32_t i);
 /* Score every pair on every context, then the top-k exchange (asynchronous on

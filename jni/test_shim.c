@@ -3,8 +3,10 @@
  * JNI shim makes, on the known-answer test of SURVEY.md §4.2, without a JDK.
  *
  *  1. always: error codes. A null options pointer, a null dataset, bad group
- *     layouts, and — on a box without a GPU — mr_create / ne_create fail with
- *     a negative code and a message (never exit, never a CPU fallback).
+ *     layouts, Java array lengths that disagree with the sizes (ne_load checks
+ *     them before the engine reads a byte), and — on a box without a GPU —
+ *     mr_create / ne_create fail with a negative code and a message (never
+ *     exit, never a CPU fallback).
  *  2. with a GPU: the single-context sequence
  *       mr_options_default -> mr_create -> mr_load -> mr_score_dense -> mr_destroy
  *     and the shim's group sequence (ne_create -> ne_load -> ne_score_dense /
@@ -54,6 +56,8 @@ static const int32_t SONG_COUNT[] = {2, 3, 3, 2};
 static const int32_t TR_LEN[] = {3, 2, 2};
 static const int32_t TE_LEN[] = {2, 1};
 enum { NTR = 3, NTE = 2, NS = 4 };
+/* Java lengths of the load arrays (tr_off, tr_songs, te_off, te_songs, song_count, tr_len, te_len) */
+static const int64_t LENS[7] = {NTR + 1, 7, NTE + 1, 3, NS, NTR, NTE};
 
 /* SURVEY.md §4.2 (NaN = heard song, no pair) */
 static const double KAT_IBM[NTE][NS] = {{NAN, 0.40824829046386296, 0.8164965809277259, NAN},
@@ -119,6 +123,22 @@ static void error_codes(void) {
   int32_t b[3];
   CHECK(mr_song_shards(&d, 2, b) == MR_OK && b[0] == 0 && b[2] == NS && b[1] > 0 && b[1] < NS, "mr_song_shards");
   CHECK(mr_song_shards(&d, NS + 1, b) == MR_E_INVALID, "more shards than songs accepted");
+  /* Java array lengths are checked before anything is read (NativeScoring's
+   * arrays, jni/mr_jni.c): each wrong length is an error naming the array */
+  static const char* arr[7] = {"trOff", "trSongs", "teOff", "teSongs", "songCount", "trLen", "teLen"};
+  for (int i = 0; i < 7; ++i) {
+    int64_t lens[7];
+    memcpy(lens, LENS, sizeof lens);
+    lens[i] -= 1;
+    CHECK(ne_load(NULL, NTR, NTE, NS, TR_OFF, TR_SONGS, TE_OFF, TE_SONGS, SONG_COUNT, TR_LEN, TE_LEN, lens) ==
+              MR_E_INVALID && strstr(ne_error(), arr[i]),
+          "short %s accepted (%s)", arr[i], ne_error());
+  }
+  CHECK(ne_load(NULL, NTR, NTE, NS, TR_OFF, TR_SONGS, TE_OFF, TE_SONGS, SONG_COUNT, TR_LEN, TE_LEN, LENS) ==
+            MR_E_INVALID && strstr(ne_error(), "handle"),
+        "null handle accepted (%s)", ne_error());
+  CHECK(ne_score_dense(NULL, MR_IBM, NULL, 0) == MR_E_INVALID, "ne_score_dense(NULL) accepted");
+  CHECK(ne_topk(NULL, MR_IBM, 3, NULL, 0, NULL, 0) == MR_E_INVALID, "ne_topk(NULL) accepted");
 }
 
 int main(void) {
@@ -156,18 +176,20 @@ int main(void) {
   for (int l = 0; l < 2; ++l) {
     const int32_t dev0 = 0;
     mr_group* g = ne_create(&dev0, 1, layouts[l][0], layouts[l][1], 3, 1);
-    CHECK(g != 0, "ne_create: %s", mr_last_error());
+    CHECK(g != 0, "ne_create: %s", ne_error());
     if (!g) continue;
-    CHECK(ne_load(g, NTR, NTE, NS, TR_OFF, TR_SONGS, TE_OFF, TE_SONGS, SONG_COUNT, TR_LEN, TE_LEN) == MR_OK,
-          "ne_load: %s", mr_last_error());
+    CHECK(ne_load(g, NTR, NTE, NS, TR_OFF, TR_SONGS, TE_OFF, TE_SONGS, SONG_COUNT, TR_LEN, TE_LEN, LENS) == MR_OK,
+          "ne_load: %s", ne_error());
     for (int model = 0; model < 2; ++model) {
-      CHECK(ne_score_dense(g, model, dense) == MR_OK, "ne_score_dense: %s", mr_last_error());
+      CHECK(ne_score_dense(g, model, dense, NTE * NS) == MR_OK, "ne_score_dense: %s", ne_error());
       check_dense(l ? "group 2x2" : "group 1x1", model, dense);
-      int32_t songs[NTE * 3];
-      double scores[NTE * 3];
-      CHECK(ne_topk(g, model, 3, songs, scores) == MR_OK, "ne_topk: %s", mr_last_error());
+      CHECK(ne_score_dense(g, model, dense, NTE * NS - 1) == MR_E_INVALID, "short dense array accepted");
+      int32_t songs[NTE * 4];
+      double scores[NTE * 4];
+      CHECK(ne_topk(g, model, 3, songs, NTE * 3, scores, NTE * 3) == MR_OK, "ne_topk: %s", ne_error());
       check_topk(l ? "group 2x2" : "group 1x1", model, 3, songs, scores);
-      CHECK(ne_topk(g, model, 4, songs, scores) == MR_E_INVALID, "k != the handle's topk accepted");
+      CHECK(ne_topk(g, model, 3, songs, NTE * 3 - 1, scores, NTE * 3) == MR_E_INVALID, "short songs array accepted");
+      CHECK(ne_topk(g, model, 4, songs, NTE * 4, scores, NTE * 4) == MR_E_INVALID, "k != the handle's topk accepted");
     }
     CHECK(ne_destroy(g) == MR_OK, "ne_destroy");
   }

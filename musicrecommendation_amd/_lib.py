@@ -179,6 +179,7 @@ SIGNATURES = {
     "mr_group_info": (c_int, [c_void_p, c_int32, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
                               POINTER(c_int32), POINTER(c_int32)]),
     "mr_group_transport": (c_int, [c_void_p, POINTER(c_int32)]),
+    "mr_group_shape": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_group_context": (c_void_p, [c_void_p, c_int32]),
     "mr_group_run": (c_int, [c_void_p, c_int]),
     "mr_group_sync": (c_int, [c_void_p]),

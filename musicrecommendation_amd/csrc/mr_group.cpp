@@ -571,6 +571,15 @@ int mr_group_transport(const mr_group* g, int32_t* transport) {
   return MR_OK;
 }
 
+int mr_group_shape(const mr_group* g, int32_t* n_contexts, int32_t* n_test, int32_t* n_songs) {
+  if (!g) return gfail(MR_E_INVALID, "null group");
+  if (!g->loaded) return gfail(MR_E_STATE, "mr_group_shape before mr_group_load");
+  if (n_contexts) *n_contexts = (int32_t)g->m.size();
+  if (n_test) *n_test = g->n_te;
+  if (n_songs) *n_songs = g->n_s;
+  return MR_OK;
+}
+
 mr_ctx* mr_group_context(mr_group* g, int32_t i) {
   if (!g || i < 0 || i >= (int)g->m.size() || !g->loaded) {
     gfail(MR_E_INVALID, "no context %d", i);
