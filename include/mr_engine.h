@@ -276,24 +276,28 @@ int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_
 /* evaluateModel (MR:636), device part: min / max over the model's scores
  * (MR:524-525; +inf / -inf when the shard holds no pair) ... */
 int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx);
-/* ... and per song s of the shard and threshold t_i = i/10 (MR:590):
+/* ... and per song s of the shard and threshold t_i = i/10, i < n_thresholds:
  * pred_counts[s][i] = #test users with (x - mn)/(mx - mn) > t_i (MR:529),
- * tp_counts[s][i] = those of them whose labels hold s (MR:545). mn/mx are the
- * GLOBAL extremes (reduce over shards first). Labels: host CSR over the
- * context's test users, global song ids (label-only songs >= n_songs). */
+ * tp_counts[s][i] = those of them whose labels hold s (MR:545). n_thresholds:
+ * 10 (0.0..0.9, evaluateModel MR:590; 0 = 10) or 11 (0.0..1.0, the distributed
+ * evaluation, distributed.scala:395). mn/mx are the GLOBAL extremes (reduce
+ * over shards first). Labels: host CSR over the context's test users, global
+ * song ids (label-only songs >= n_songs). Counts: [width][n_thresholds]. */
 int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts);
-/* Host part: AP per song class (MR:588-618, left folds as List.sum) and mAP =
- * sum / n_label_songs (MR:625-627), classes summed in song-id order. pos[s] =
- * #test users whose labels hold s. */
+                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts, int32_t n_thresholds);
+/* Host part: AP per song class (MR:588-618, left folds as List.sum; with 11
+ * thresholds distributed.scala:401-415) and mAP = sum / n_label_songs
+ * (MR:625-627), classes summed in song-id order (the distributed version sums
+ * with RDD.sum, in partition order). pos[s] = #test users whose labels hold s. */
 int mr_eval_map(int32_t n_classes, const int32_t* pred_counts, const int32_t* tp_counts, const int32_t* pos,
-                int32_t n_label_songs, double* map_out);
+                int32_t n_label_songs, double* map_out, int32_t n_thresholds);
 /* The two above in one call for a context that holds every test user: counts
  * and the per-class AP on the device (the same double operations), only the
  * AP per class crosses PCIe, summed on the host in song-id order — bit-equal
  * to mr_eval_counts_device + mr_eval_map. pos: host [>= song_hi], global. */
 int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out);
+                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out,
+                       int32_t n_thresholds);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
  * (0 = separate stage-1 kernel — neighbour lists —, 1 = the

@@ -155,10 +155,11 @@ SIGNATURES = {
     "mr_topk_dense_device": (c_int, [c_void_p, c_void_p, c_int32]),
     "mr_combine_device": (c_int, [c_void_p, c_int, c_double, ctypes.c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "mr_eval_minmax_device": (c_int, [c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)]),
-    "mr_eval_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mr_eval_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_int32]),
     "mr_eval_map_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_int32,
-                                   POINTER(c_double)]),
-    "mr_eval_map": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double)]),
+                                   POINTER(c_double), c_int32]),
+    "mr_eval_map": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double), c_int32]),
     "mr_last_error": (c_char_p, []),
     "mr_corpus_from_tsv": (c_int, [c_char_p, c_char_p, c_char_p, POINTER(c_void_p)]),
     "mr_corpus_dataset": (c_int, [c_void_p, POINTER(MrDataset)]),

@@ -7,8 +7,10 @@
 //                                     reference's java.util.Random is unseeded, here a
 //                                     seeded counter-based stream over the pair index
 //   evaluateModel                     MR:521-639  global min/max (MR:524-525), per-class
-//                                     confusion counts at the 10 thresholds (MR:541-553,
-//                                     MR:590); AP and the mean on the host (mr_eval_map)
+//                                     confusion counts at the thresholds (MR:541-553):
+//                                     0.0..0.9 (10, MR:590) or 0.0..1.0 (11, the
+//                                     distributed evaluation, distributed.scala:395);
+//                                     AP per class and the mean (mr_eval_map[_device])
 // The pair index is the position of (u, s) in the driver's sorted model
 // (main.scala:57-59 sorts by (user, song): the interned order, heard songs
 // skipped): idx(u, s) = pair_base + u*n_s - te_off[u] + s - |{t in T(u): t < s}|.
@@ -38,10 +40,15 @@ using mr_host::fail;
   } while (0)
 
 constexpr int kThreads = 256;
-constexpr int kThresholds = 10;  // 0.0, 0.1, ..., 0.9 (MR:590)
-#define MR_THRESHOLDS {0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9}
+// Thresholds: the first n of 0.0, 0.1, ..., 1.0 — n = 10 for MusicRecommender's
+// evaluateModel (MR:590: 0.0 :: ... :: 0.9 :: Nil), n = 11 for the distributed
+// evaluation (distributed.scala:395: Array(0.0, ..., 1.0)); the same literals.
+constexpr int kThresholds = 11;  // the most any evaluation uses
+#define MR_THRESHOLDS {0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0}
 __constant__ double kThr[kThresholds] = MR_THRESHOLDS;
 constexpr double kThrHost[kThresholds] = MR_THRESHOLDS;
+
+inline int thresholds_or_default(int n) { return n == 0 ? 10 : n; }
 
 // ---- combination models -----------------------------------------------------
 struct CombParams {
@@ -162,11 +169,11 @@ __global__ __launch_bounds__(kThreads) void k_minmax(const OutT* d, long long n,
 }
 
 struct EvalParams {
-  int n_te, width, song_lo, users_per_block;
+  int n_te, width, song_lo, users_per_block, n_thr;
   double mn, mx;
   const void* dense;
-  int* pred;  // [width][10]: users with (x - min) / (max - min) > t_i (MR:529)
-  int* tp;    // [width][10]: of those, users whose labels hold the song (MR:545)
+  int* pred;  // [width][n_thr]: users with (x - min) / (max - min) > t_i (MR:529)
+  int* tp;    // [width][n_thr]: of those, users whose labels hold the song (MR:545)
   const int* lab_u;
   const int* lab_s;
   long long n_lab;
@@ -179,7 +186,7 @@ struct EvalParams {
 // so it equals x >= xt with xt the smallest score of the model's element type
 // that passes. Found on the host by bisection over the ordered bit patterns of
 // that type, with the same fp64 expression: exact, and the kernel then needs
-// 10 compares per element instead of an fp64 division.
+// n_thr compares per element instead of an fp64 division.
 template <typename T, typename U>
 T level_floor(double mn, double mx, double t) {
   constexpr int B = sizeof(T) * 8;
@@ -196,11 +203,11 @@ T level_floor(double mn, double mx, double t) {
   return val(lo);
 }
 
-__device__ __forceinline__ int levels(double x, double mn, double mx) {
+__device__ __forceinline__ int levels(double x, double mn, double mx, int n_thr) {
   const double v = (x - mn) / (mx - mn);  // MR:529 (NaN > t is false)
   int c = 0;
 #pragma unroll
-  for (int t = 0; t < kThresholds; ++t) c += v > kThr[t] ? 1 : 0;
+  for (int t = 0; t < kThresholds; ++t) c += (t < n_thr && v > kThr[t]) ? 1 : 0;
   return c;  // thresholds ascend: predicted at t_i for every i < c
 }
 
@@ -213,7 +220,8 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   const OutT* d = reinterpret_cast<const OutT*>(p.dense);
   OutT xt[kThresholds];
 #pragma unroll
-  for (int t = 0; t < kThresholds; ++t) xt[t] = sizeof(OutT) == 4 ? (OutT)p.xt_f[t] : (OutT)p.xt_d[t];
+  for (int t = 0; t < kThresholds; ++t)  // unused slots: +inf, never reached
+    xt[t] = t < p.n_thr ? (sizeof(OutT) == 4 ? (OutT)p.xt_f[t] : (OutT)p.xt_d[t]) : (OutT)INFINITY;
   int cnt[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) cnt[t] = 0;
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   }
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t)
-    if (cnt[t]) atomicAdd(&p.pred[(size_t)i * kThresholds + t], cnt[t]);
+    if (cnt[t]) atomicAdd(&p.pred[(size_t)i * p.n_thr + t], cnt[t]);
 }
 
 template <typename OutT>
@@ -240,15 +248,15 @@ __global__ __launch_bounds__(kThreads) void k_eval_tp(EvalParams p) {
   if (g < 0 || g >= p.width) return;  // other shard, or a label-only song (never predicted)
   const double x = (double)reinterpret_cast<const OutT*>(p.dense)[(size_t)u * p.width + g];
   if (x != x) return;
-  const int c = levels(x, p.mn, p.mx);
-  for (int t = 0; t < c; ++t) atomicAdd(&p.tp[(size_t)g * kThresholds + t], 1);
+  const int c = levels(x, p.mn, p.mx, p.n_thr);
+  for (int t = 0; t < c; ++t) atomicAdd(&p.tp[(size_t)g * p.n_thr + t], 1);
 }
 
 // AP of the label classes cls[0..n) of the shard (shard-local song ids, np =
 // their label counts pos, all > 0; MR:588-618), the host fold's exact double
 // operations (mr_eval_map) per class.
-__global__ __launch_bounds__(kThreads) void k_eval_ap(int n, const int* cls, const int* cpos, const int* pred,
-                                                      const int* tp, double* ap) {
+__global__ __launch_bounds__(kThreads) void k_eval_ap(int n, int n_thr, const int* cls, const int* cpos,
+                                                      const int* pred, const int* tp, double* ap) {
   const int c = blockIdx.x * kThreads + threadIdx.x;
   if (c >= n) return;
   const int g = cls[c];
@@ -256,14 +264,17 @@ __global__ __launch_bounds__(kThreads) void k_eval_ap(int n, const int* cls, con
   double P[kThresholds], R[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) {
-    const size_t i = (size_t)g * kThresholds + t;
+    const size_t i = (size_t)g * n_thr + (t < n_thr ? t : 0);
     P[t] = pred[i] > 0 ? (double)tp[i] / (double)pred[i] : 0.0;
     R[t] = (double)tp[i] / (double)np;
   }
+  // AP = sum over i of: (R_i - R_{i+1}) * P_i, (R_{n-2} - 0.0) * P_{n-2} at
+  // i = n - 2, 0 at i = n - 1 (MR:601-609, distributed.scala:405-413), left fold
   double a = 0.0;
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) {
-    const double term = t == 9 ? 0.0 : t == 8 ? (R[8] - 0.0) * P[8] : (R[t] - R[t + 1]) * P[t];
+    if (t >= n_thr) break;
+    const double term = t == n_thr - 1 ? 0.0 : t == n_thr - 2 ? (R[t] - 0.0) * P[t] : (R[t] - R[t + 1]) * P[t];
     a = a + term;
   }
   ap[c] = a;
@@ -277,10 +288,12 @@ struct Tmp {  // scratch device buffer of one call, stream-ordered (pool allocat
 };
 
 // pred / tp counts of the shard into the device buffers d_pred / d_tp
-// ([width][10], stream-ordered on the context stream; the caller frees them).
+// ([width][n_thr], stream-ordered on the context stream; the caller frees them).
 int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                const int32_t* lab_songs, mr_view& v, Tmp<int>& d_pred, Tmp<int>& d_tp) {
+                const int32_t* lab_songs, int n_thr, mr_view& v, Tmp<int>& d_pred, Tmp<int>& d_tp) {
   if (!ctx || !dense || !lab_off) return fail(MR_E_INVALID, "null argument");
+  if (n_thr != 10 && n_thr != 11)
+    return fail(MR_E_INVALID, "%d thresholds: 10 (MR:590) or 11 (distributed.scala:395)", n_thr);
   int rc = mr_view_get(ctx, &v);
   if (rc) return rc;
   MR_HIP(hipSetDevice(v.device));
@@ -297,7 +310,7 @@ int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int6
   hipStream_t st = (hipStream_t)v.stream;
   Tmp<int> d_lu, d_ls;
   d_pred.st = d_tp.st = d_lu.st = d_ls.st = st;
-  const size_t nc = (size_t)width * kThresholds;
+  const size_t nc = (size_t)width * n_thr;
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_pred.p), std::max<size_t>(1, nc) * 4, st));
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_tp.p), std::max<size_t>(1, nc) * 4, st));
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_lu.p), lu.size() * 4, st));
@@ -309,10 +322,10 @@ int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int6
   // enough (song block x user block) workgroups to fill the chip
   const int sx = (width + kThreads - 1) / kThreads;
   const int uy = std::max(1, std::min((n_te + 31) / 32, (8192 + sx - 1) / sx));
-  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p, d_ls.p,
-                n_lab};
+  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, n_thr, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p,
+                d_ls.p, n_lab};
   const bool f64 = v.out_dtype == MR_OUT_F64;
-  for (int t = 0; t < kThresholds; ++t) {
+  for (int t = 0; t < n_thr; ++t) {
     const double thr = kThrHost[t];
     ep.xt_f[t] = level_floor<float, uint32_t>(mn, mx, thr);
     ep.xt_d[t] = level_floor<double, uint64_t>(mn, mx, thr);
@@ -404,14 +417,15 @@ int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx
 }
 
 int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts) {
+                          const int32_t* lab_songs, int32_t* pred_counts, int32_t* tp_counts, int32_t n_thresholds) {
   if (!pred_counts || !tp_counts) return fail(MR_E_INVALID, "null argument");
+  const int n_thr = thresholds_or_default(n_thresholds);
   mr_view v;
   Tmp<int> d_pred, d_tp;
-  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, v, d_pred, d_tp);
+  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)v.stream;
-  const size_t nc = (size_t)(v.song_hi - v.song_lo) * kThresholds;
+  const size_t nc = (size_t)(v.song_hi - v.song_lo) * n_thr;
   MR_HIP(hipMemcpyAsync(pred_counts, d_pred.p, nc * 4, hipMemcpyDeviceToHost, st));
   MR_HIP(hipMemcpyAsync(tp_counts, d_tp.p, nc * 4, hipMemcpyDeviceToHost, st));
   MR_HIP(hipStreamSynchronize(st));
@@ -419,11 +433,13 @@ int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, 
 }
 
 int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out) {
+                       const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out,
+                       int32_t n_thresholds) {
   if (!pos || !map_out) return fail(MR_E_INVALID, "null argument");
+  const int n_thr = thresholds_or_default(n_thresholds);
   mr_view v;
   Tmp<int> d_pred, d_tp;
-  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, v, d_pred, d_tp);
+  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)v.stream;
   const int width = v.song_hi - v.song_lo;
@@ -443,7 +459,7 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
     MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)nc * 8, st));
     MR_HIP(hipMemcpyAsync(d_cls.p, cls.data(), (size_t)nc * 4, hipMemcpyHostToDevice, st));
     MR_HIP(hipMemcpyAsync(d_cpos.p, cpos.data(), (size_t)nc * 4, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_eval_ap, dim3((nc + kThreads - 1) / kThreads), dim3(kThreads), 0, st, nc, d_cls.p,
+    hipLaunchKernelGGL(k_eval_ap, dim3((nc + kThreads - 1) / kThreads), dim3(kThreads), 0, st, nc, n_thr, d_cls.p,
                        d_cpos.p, d_pred.p, d_tp.p, d_ap.p);
     MR_HIP(hipGetLastError());
     MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)nc * 8, hipMemcpyDeviceToHost, st));

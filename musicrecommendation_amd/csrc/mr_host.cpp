@@ -697,20 +697,22 @@ int mr_topk_merge_host(int32_t n_shards, int32_t n_te, int32_t k, const int32_t*
 }
 
 int mr_eval_map(int32_t n_classes, const int32_t* pred, const int32_t* tp, const int32_t* pos,
-                int32_t n_label_songs, double* map_out) {
+                int32_t n_label_songs, double* map_out, int32_t n_thresholds) {
   if (!pred || !tp || !pos || !map_out || n_classes < 0) return mr_host::fail(MR_E_INVALID, "bad argument");
+  const int T = n_thresholds == 0 ? 10 : n_thresholds;  // 10: MR:590; 11: distributed.scala:395
+  if (T != 10 && T != 11) return mr_host::fail(MR_E_INVALID, "%d thresholds: 10 or 11", n_thresholds);
   double total = 0.0;
   for (int g = 0; g < n_classes; ++g) {
     if (pos[g] <= 0) continue;  // AP = 0 for classes nobody holds
-    double P[10], R[10];
-    for (int t = 0; t < 10; ++t) {
-      const size_t i = (size_t)g * 10 + t;
+    double P[11], R[11];
+    for (int t = 0; t < T; ++t) {
+      const size_t i = (size_t)g * T + t;
       P[t] = pred[i] > 0 ? (double)tp[i] / (double)pred[i] : 0.0;  // precision, MR:563-568
       R[t] = (double)tp[i] / (double)pos[g];                        // recall, MR:576-581
     }
-    double ap = 0.0;  // MR:601-609, summed left to right
-    for (int t = 0; t < 10; ++t) {
-      const double term = t == 9 ? 0.0 : t == 8 ? (R[8] - 0.0) * P[8] : (R[t] - R[t + 1]) * P[t];
+    double ap = 0.0;  // MR:601-609 / distributed.scala:405-413, summed left to right
+    for (int t = 0; t < T; ++t) {
+      const double term = t == T - 1 ? 0.0 : t == T - 2 ? (R[t] - 0.0) * P[t] : (R[t] - R[t + 1]) * P[t];
       ap = ap + term;
     }
     total += ap;

@@ -203,24 +203,26 @@ class Engine:
 
     def eval_counts(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray,
                     lab_songs: np.ndarray, pred: Optional[np.ndarray] = None,
-                    tp: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
-        """(pred, tp) counts, each width x 10 int32 (MR:529, MR:541-553); pred / tp
-        may be caller-owned (e.g. pinned) C-contiguous int32 width x 10 arrays."""
+                    tp: Optional[np.ndarray] = None, n_thresholds: int = 10) -> Tuple[np.ndarray, np.ndarray]:
+        """(pred, tp) counts, each width x n_thresholds int32 (MR:529, MR:541-553;
+        10 thresholds = MR:590, 11 = distributed.scala:395); pred / tp may be
+        caller-owned (e.g. pinned) C-contiguous int32 arrays of that shape."""
         lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
         lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
+        shape = (self.width, n_thresholds)
         for a in (pred, tp):
-            if a is not None and (a.dtype != np.int32 or a.shape != (self.width, 10) or not a.flags.c_contiguous):
-                raise ValueError("pred / tp must be C-contiguous int32 arrays of shape (width, 10)")
-        pred = np.empty((self.width, 10), dtype=np.int32) if pred is None else pred
-        tp = np.empty((self.width, 10), dtype=np.int32) if tp is None else tp
+            if a is not None and (a.dtype != np.int32 or a.shape != shape or not a.flags.c_contiguous):
+                raise ValueError(f"pred / tp must be C-contiguous int32 arrays of shape {shape}")
+        pred = np.empty(shape, dtype=np.int32) if pred is None else pred
+        tp = np.empty(shape, dtype=np.int32) if tp is None else tp
         _lib.check(self._L.mr_eval_counts_device(
             self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
             lab_songs.ctypes.data_as(ctypes.c_void_p), pred.ctypes.data_as(ctypes.c_void_p),
-            tp.ctypes.data_as(ctypes.c_void_p)), "mr_eval_counts_device")
+            tp.ctypes.data_as(ctypes.c_void_p), int(n_thresholds)), "mr_eval_counts_device")
         return pred, tp
 
     def eval_map(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray, lab_songs: np.ndarray,
-                 pos: np.ndarray, n_label_songs: int) -> float:
+                 pos: np.ndarray, n_label_songs: int, n_thresholds: int = 10) -> float:
         """Threshold mAP with counts and per-class AP on the device
         (mr_eval_map_device; the context must hold every test user)."""
         lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
@@ -232,7 +234,7 @@ class Engine:
         _lib.check(self._L.mr_eval_map_device(
             self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
             lab_songs.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p), int(n_label_songs),
-            ctypes.byref(out)), "mr_eval_map_device")
+            ctypes.byref(out), int(n_thresholds)), "mr_eval_map_device")
         return out.value
 
     def timing_begin(self) -> None:

@@ -40,14 +40,15 @@ def pair_uniform(seed: int, idx: int) -> float:
 
 
 def eval_map(pred: np.ndarray, tp: np.ndarray, pos: np.ndarray, n_label_songs: int) -> float:
-    """mAP from the per-class counts (mr_eval_map, MR:588-627)."""
+    """mAP from the per-class counts (mr_eval_map, MR:588-627; the threshold
+    count is pred.shape[1]: 10 = MR:590, 11 = distributed.scala:395)."""
     pred = np.ascontiguousarray(pred, dtype=np.int32)
     tp = np.ascontiguousarray(tp, dtype=np.int32)
     pos = np.ascontiguousarray(pos, dtype=np.int32)
     out = ctypes.c_double()
     _lib.check(_lib.lib().mr_eval_map(pred.shape[0], pred.ctypes.data_as(ctypes.c_void_p),
                                       tp.ctypes.data_as(ctypes.c_void_p), pos.ctypes.data_as(ctypes.c_void_p),
-                                      int(n_label_songs), ctypes.byref(out)), "mr_eval_map")
+                                      int(n_label_songs), ctypes.byref(out), int(pred.shape[1])), "mr_eval_map")
     return out.value
 
 
@@ -130,8 +131,9 @@ class DeviceEnsemble:
 
         return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
 
-    def threshold_map(self, t) -> float:
-        """evaluateModel (MR:636) of a dense device model."""
+    def threshold_map(self, t, n_thresholds: int = 10) -> float:
+        """evaluateModel (MR:636) of a dense device model; n_thresholds = 11 is
+        the distributed evaluation (distributed.scala:395)."""
         import torch
         import torch.distributed as dist
 
@@ -151,16 +153,18 @@ class DeviceEnsemble:
         if world == 1 and self.e.song_lo == 0 and self.e.song_hi == self.ds.n_songs and hasattr(self.e, "eval_map"):
             # one context holds the whole model: counts, AP per class on the device
             return self.e.eval_map(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, self.pos,
-                                   self.n_label_songs)
-        if self._host is None and torch.cuda.is_available():  # pinned, reused: no page faults per call
-            self._host = [torch.empty((self.e.width, 10), dtype=torch.int32, pin_memory=True).numpy()
+                                   self.n_label_songs, n_thresholds=n_thresholds)
+        if (self._host is None or self._host[0].shape[1] != n_thresholds) and torch.cuda.is_available():
+            # pinned, reused: no page faults per call
+            self._host = [torch.empty((self.e.width, n_thresholds), dtype=torch.int32, pin_memory=True).numpy()
                           for _ in range(2)]
         bufs = {} if self._host is None else {"pred": self._host[0], "tp": self._host[1]}
-        pred, tp = self.e.eval_counts(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, **bufs)
+        pred, tp = self.e.eval_counts(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs,
+                                      n_thresholds=n_thresholds, **bufs)
         if self.e.song_lo == 0 and self.e.song_hi == self.ds.n_songs:
             full_p, full_t = pred, tp
         else:
-            full_p = np.zeros((self.ds.n_songs, 10), dtype=np.int32)
+            full_p = np.zeros((self.ds.n_songs, n_thresholds), dtype=np.int32)
             full_t = np.zeros_like(full_p)
             full_p[self.e.song_lo:self.e.song_hi] = pred
             full_t[self.e.song_lo:self.e.song_hi] = tp

@@ -16,6 +16,8 @@ import numpy as np
 from .dataset import Dataset
 
 THRESHOLDS = (0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9)  # MR:590
+# the distributed evaluation's 11 thresholds (distributed.scala:395)
+THRESHOLDS_DISTRIBUTED = THRESHOLDS + (1.0,)
 
 
 def label_matrix(ds: Dataset) -> np.ndarray:
@@ -33,7 +35,7 @@ def label_pos(ds: Dataset) -> np.ndarray:
 
 
 def threshold_counts(scores: np.ndarray, ds: Dataset, mn: float, mx: float, thresholds=THRESHOLDS):
-    """(pred, tp), each n_songs x 10: per song and threshold, the test users
+    """(pred, tp), each n_songs x len(thresholds): per song and threshold, the test users
     predicted ((x - mn)/(mx - mn) > t, MR:529) and those of them whose labels
     hold the song (MR:541-553). The numpy twin of mr_eval_counts_device."""
     x = np.asarray(scores, dtype=np.float64)
@@ -53,8 +55,10 @@ def threshold_counts(scores: np.ndarray, ds: Dataset, mn: float, mx: float, thre
 
 def map_from_counts(pred: np.ndarray, tp: np.ndarray, pos: np.ndarray, n_label_songs: int) -> float:
     """AP per class (MR:588-618) and the mean (MR:625-627) from the counts:
-    P_i = TP/(TP+FP), R_i = TP/(TP+FN) (MR:563-581), AP = Σ_{i<8} (R_i−R_{i+1})·P_i
-    + R_8·P_8 + 0 (left fold), classes summed in song-id order."""
+    P_i = TP/(TP+FP), R_i = TP/(TP+FN) (MR:563-581), with n = pred.shape[1]
+    thresholds AP = Σ_{i<n-2} (R_i−R_{i+1})·P_i + R_{n-2}·P_{n-2} + 0 (left
+    fold; n = 10 MR:601-609, n = 11 distributed.scala:405-413), classes summed
+    in song-id order."""
     if n_label_songs == 0:
         return float("nan")
     pred = np.asarray(pred, dtype=np.float64)

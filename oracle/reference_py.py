@@ -191,9 +191,12 @@ class LiteralRecommender:
         return cm[0] / (cm[0] + cm[3]) if cm[0] + cm[3] > 0 else 0.0
 
     THRESHOLDS = [0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9]  # MR:590
+    THRESHOLDS_DISTRIBUTED = [0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0]  # distributed.scala:395
 
-    def average_precision(self, model: Model) -> List[Tuple[str, float]]:
-        ths = self.THRESHOLDS
+    def average_precision(self, model: Model, thresholds=None) -> List[Tuple[str, float]]:
+        """MR:588-618 (thresholds=None); with THRESHOLDS_DISTRIBUTED the same
+        recurrence over 11 thresholds, distributed.scala:394-416."""
+        ths = self.THRESHOLDS if thresholds is None else thresholds
         preds = [self.prediction_to_class_labels(model, t) for t in ths]
         out = []
         for song in self.new_songs:
@@ -214,9 +217,11 @@ class LiteralRecommender:
             out.append((song, acc))
         return out
 
-    def evaluate_model(self, model: Model) -> float:
+    def evaluate_model(self, model: Model, thresholds=None) -> float:
+        """MR:625-639 (foldLeft over newSongs); distributed.scala:424-442 sums
+        with RDD.sum (partition order) over the same values."""
         acc = 0.0
-        for _s, ap in self.average_precision(model):
+        for _s, ap in self.average_precision(model, thresholds):
             acc += ap
         return acc / len(self.new_songs)
 

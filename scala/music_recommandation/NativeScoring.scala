@@ -59,10 +59,22 @@ trait NativeScoring {
     h
   }
 
-  /** getModel(rank) for rank = UBM / IBM: every (test user, unheard song) pair. */
+  /** getModel(rank) for rank = UBM / IBM: every (test user, unheard song) pair.
+   *
+   * The dense model has nTe x nS cells, one JVM array: above Int.MaxValue cells
+   * (the full Taste Profile: 10,000 x 384,546 = 3.85e9) neither it nor the
+   * reference's pair array can exist, so the size is computed as a Long and such
+   * a request fails with a clear exception instead of wrapping negative; use
+   * nativeRecommendations (top-k lists) at that scale. Indices below stay Int:
+   * they are < nTe * nS <= Int.MaxValue. */
   def nativeModel(model: Int): Array[(String, (String, Double))] = {
     val nS = songIds.length
-    val out = new Array[Double](teIds.length * nS)
+    val cells = teIds.length.toLong * nS
+    if (cells > Int.MaxValue - 8)  // the JVM's largest array
+      throw new IllegalArgumentException(
+        s"dense model of ${teIds.length} test users x $nS songs = $cells cells exceeds a JVM array; " +
+        "use nativeRecommendations(model) for the per-user top-k lists")
+    val out = new Array[Double](cells.toInt)
     NativeEngine.scoreDense(handle, model, out)
     for {
       s <- songs

@@ -1,7 +1,9 @@
 """Combination models and the threshold mAP, host side (no GPU):
 * the stochastic model's seeded stream: product restatement = oracle restatement;
 * the mAP fold of the counts (C mr_eval_map and numpy map_from_counts) = the
-  literal restatement of MR:521-639 (oracle/reference_py.py) on the fixtures;
+  literal restatement of MR:521-639 (oracle/reference_py.py) on the fixtures,
+  with MR's 10 thresholds and with the distributed evaluation's 11
+  (distributed.scala:395-415);
 * the Model-array API mirror (MR:317-481) = the oracle's literal versions;
 * the multi-rank reduction of DeviceEnsemble.threshold_map (gloo, world 2)
   over song shards and over test-user blocks = the single-process value."""
@@ -53,9 +55,11 @@ def _dense_of(ds, model):
     return d
 
 
+@pytest.mark.parametrize("n_thr", [10, 11])
 @pytest.mark.parametrize("name", ["kat", "tiny", "small"])
 @pytest.mark.parametrize("model", MODELS)
-def test_map_fold_matches_literal_evaluation(name, model):
+def test_map_fold_matches_literal_evaluation(name, model, n_thr):
+    ths = evaluation.THRESHOLDS if n_thr == 10 else evaluation.THRESHOLDS_DISTRIBUTED
     lr, ds = _literal(name)
     if name == "kat":
         m = lr.get_item_based_model() if model == "ibm" else lr.get_user_based_model()
@@ -64,15 +68,32 @@ def test_map_fold_matches_literal_evaluation(name, model):
         dense = synth_fixture(name)[1][model]
         m = [(ds.test_names(u), (ds.song_names(s), float(dense[u, s])))
              for s in range(ds.n_songs) for u in range(ds.n_test) if not np.isnan(dense[u, s])]
-    ref = lr.evaluate_model(m)
-    host = evaluation.threshold_map(dense, ds)
+    ref = lr.evaluate_model(m, list(ths))
+    host = evaluation.threshold_map(dense, ds, ths)
     valid = ~np.isnan(dense)
-    pred, tp = evaluation.threshold_counts(dense, ds, dense[valid].min(), dense[valid].max())
+    pred, tp = evaluation.threshold_counts(dense, ds, dense[valid].min(), dense[valid].max(), ths)
+    assert pred.shape[1] == n_thr
     c_map = eval_map(pred, tp, evaluation.label_pos(ds), ds.n_label_songs)
     assert c_map == host                       # C fold == numpy fold, bit for bit
     assert abs(host - ref) <= 1e-12            # == literal MR:521-639 (class order: ulps)
     if name == "kat":
-        assert abs(host - 0.6666666666666666) < 1e-15
+        assert abs(host - 0.6666666666666666) < 1e-15  # SURVEY.md §4.2 (10 and 11 thresholds)
+
+
+def test_eleven_thresholds_differ_from_ten():
+    """The 11-threshold recurrence is not the 10-threshold one (it adds the
+    (R_8 - R_9) P_8 + R_9 P_9 tail): on a fixture with mid-range scores the two
+    mAPs differ, each equal to its literal restatement."""
+    lr, ds = _literal("small")
+    dense = synth_fixture("small")[1]["ibm"]
+    m = [(ds.test_names(u), (ds.song_names(s), float(dense[u, s])))
+         for s in range(ds.n_songs) for u in range(ds.n_test) if not np.isnan(dense[u, s])]
+    a = evaluation.threshold_map(dense, ds, evaluation.THRESHOLDS)
+    b = evaluation.threshold_map(dense, ds, evaluation.THRESHOLDS_DISTRIBUTED)
+    assert a != b
+    assert abs(b - lr.evaluate_model(m, lr.THRESHOLDS_DISTRIBUTED)) <= 1e-12
+    with pytest.raises(Exception):
+        eval_map(np.zeros((3, 9), np.int32), np.zeros((3, 9), np.int32), np.ones(3, np.int32), 3)
 
 
 @pytest.mark.parametrize("name", ["kat", "tiny"])
@@ -107,8 +128,9 @@ class _HostEngine:
         v = x[~np.isnan(x)]
         return (float(v.min()), float(v.max())) if v.size else (np.inf, -np.inf)
 
-    def eval_counts(self, _ptr, mn, mx, lab_off, lab_songs):
-        p, t = evaluation.threshold_counts(self.dense, self.dataset, mn, mx)
+    def eval_counts(self, _ptr, mn, mx, lab_off, lab_songs, n_thresholds=10, **_bufs):
+        ths = evaluation.THRESHOLDS if n_thresholds == 10 else evaluation.THRESHOLDS_DISTRIBUTED
+        p, t = evaluation.threshold_counts(self.dense, self.dataset, mn, mx, ths)
         return p[self.song_lo:self.song_hi].astype(np.int32), t[self.song_lo:self.song_hi].astype(np.int32)
 
 
@@ -118,7 +140,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, layout, out):
+def _worker(rank, world, port, layout, out, n_thr=10):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -144,18 +166,19 @@ def _worker(rank, world, port, layout, out):
         class _Ptr:  # the host stand-in ignores the device pointer
             def data_ptr(self):
                 return 0
-        out[rank] = ens.threshold_map(_Ptr())
+        out[rank] = ens.threshold_map(_Ptr(), n_thresholds=n_thr)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("layout", ["songs", "users", "2d"])
-def test_gloo_world2_threshold_map_reduction(layout):
+@pytest.mark.parametrize("layout,n_thr", [("songs", 10), ("users", 10), ("2d", 10), ("songs", 11)])
+def test_gloo_world2_threshold_map_reduction(layout, n_thr):
     world = 4 if layout == "2d" else 2
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, _free_port(), layout, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), layout, out, n_thr), nprocs=world, join=True)
         res = dict(out)
     ds, z = synth_fixture("small")
-    ref = evaluation.threshold_map(z["ibm"], ds)
+    ref = evaluation.threshold_map(z["ibm"], ds,
+                                   evaluation.THRESHOLDS if n_thr == 10 else evaluation.THRESHOLDS_DISTRIBUTED)
     assert all(res[r] == ref for r in range(world))

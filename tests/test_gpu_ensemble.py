@@ -193,21 +193,30 @@ def test_level_thresholds_exact_at_boundaries(dtype):
         assert ens.threshold_map(t) == evaluation.threshold_map(xd, ds)
 
 
+@pytest.mark.parametrize("n_thr", [10, 11])
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_device_map_fold_equals_host_fold(dtype):
+def test_device_map_fold_equals_host_fold(dtype, n_thr):
     """mr_eval_map_device (counts + AP per class on the device, ordered host sum)
-    == mr_eval_counts_device + mr_eval_map, bit for bit, and both == numpy."""
+    == mr_eval_counts_device + mr_eval_map, bit for bit, and both == numpy;
+    with MR's 10 thresholds and the distributed evaluation's 11
+    (distributed.scala:395), whose counts also equal numpy's column for column."""
     from musicrecommendation_amd.ensemble import eval_map
 
+    ths = evaluation.THRESHOLDS if n_thr == 10 else evaluation.THRESHOLDS_DISTRIBUTED
     for name, ds in datasets():
         with Engine(ds, out_dtype=dtype, topk=4) as e:
             ens = DeviceEnsemble(e)
             for t in (ens.model("ubm"), ens.model("ibm")):
                 mn, mx = e.eval_minmax(t.data_ptr())
-                pred, tp = e.eval_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs)
+                pred, tp = e.eval_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, n_thresholds=n_thr)
+                x = t.cpu().numpy().astype(np.float64)
+                np_pred, np_tp = evaluation.threshold_counts(x, ds, mn, mx, ths)
+                assert np.array_equal(pred, np_pred) and np.array_equal(tp, np_tp), name
                 host = eval_map(pred, tp, ens.pos, ds.n_label_songs)
-                dev = e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, ens.pos, ds.n_label_songs)
+                dev = e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, ens.pos, ds.n_label_songs,
+                                 n_thresholds=n_thr)
                 assert dev == host, name
-                assert dev == evaluation.threshold_map(t.cpu().numpy().astype(np.float64), ds), name
+                assert dev == evaluation.threshold_map(x, ds, ths), name
+                assert ens.threshold_map(t, n_thresholds=n_thr) == dev, name
             with pytest.raises(ValueError):
                 e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, ens.pos[:1], ds.n_label_songs)
