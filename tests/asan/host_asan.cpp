@@ -96,7 +96,11 @@ int main(int argc, char** argv) {
   const int32_t tp[2 * 10] = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   const int32_t pos[2] = {1, 2};
   double map = -1;
-  CHECK(mr_eval_map(2, pred, tp, pos, 3, &map) == MR_OK && map >= 0 && map <= 1);
+  CHECK(mr_eval_map(2, pred, tp, pos, 3, &map, 10) == MR_OK && map >= 0 && map <= 1);
+  const int32_t pred11[2 * 11] = {3, 3, 2, 2, 1, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0};
+  const int32_t tp11[2 * 11] = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  CHECK(mr_eval_map(2, pred11, tp11, pos, 3, &map, 11) == MR_OK && map >= 0 && map <= 1);
+  CHECK(mr_eval_map(2, pred11, tp11, pos, 3, &map, 12) == MR_E_INVALID);
   std::printf("host asan: %s\n", failures ? "FAIL" : "ok");
   return failures ? 1 : 0;
 }
