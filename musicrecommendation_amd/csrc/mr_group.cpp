@@ -656,15 +656,19 @@ int mr_group_copy_dense(mr_group* g, void* out) {
   if (!g->ran) return gfail(MR_E_STATE, "no mr_group_run yet");
   if (!g->opt.dense) return gfail(MR_E_STATE, "group created with dense=0");
   const size_t e = g->esz();
+  if (int rc = sync_all(g)) return rc;
+  // one context at a time through its pinned staging (d2h_staged): the
+  // host threads of the staged copy serve one transfer at once
   for (auto& x : g->m) {
     const void* src = member_dense(g, x);
     if (!src) return gfail(MR_E_STATE, "context without a dense model");
     const size_t w = (size_t)(x.song_hi - x.song_lo);
     G_HIP(hipSetDevice(x.dev));
-    G_HIP(hipMemcpy2DAsync(static_cast<char*>(out) + ((size_t)x.user_lo * g->n_s + x.song_lo) * e, (size_t)g->n_s * e,
-                           src, w * e, w * e, (size_t)(x.user_hi - x.user_lo), hipMemcpyDeviceToHost, x.stream));
+    if (int rc = mr_internal::d2h_staged(x.ctx, static_cast<char*>(out) + ((size_t)x.user_lo * g->n_s + x.song_lo) * e,
+                                         (size_t)g->n_s * e, src, w * e, w * e, (size_t)(x.user_hi - x.user_lo)))
+      return rc;
   }
-  return sync_all(g);
+  return MR_OK;
 }
 
 int mr_group_score_dense(mr_group* g, int model, void* out) {

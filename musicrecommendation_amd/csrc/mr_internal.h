@@ -3,6 +3,7 @@
 #ifndef MR_INTERNAL_H
 #define MR_INTERNAL_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "mr_engine.h"
@@ -26,6 +27,10 @@ int topk_records(mr_ctx* c, void** records, int64_t* rec_bytes);
 // mr_load's input checks (CSR shapes, sorted rows, id ranges, counts) without
 // loading: what mr_group_load runs before it reads the dataset itself.
 int validate_dataset(const mr_dataset* d);
+
+// Synchronous device -> host copy of rows (pitched), staged through the
+// context's pinned buffers when the destination is large pageable memory.
+int d2h_staged(mr_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch, size_t row_bytes, size_t rows);
 
 // Set the calling thread's mr_last_error() message; returns code.
 int set_error(int code, const char* msg);

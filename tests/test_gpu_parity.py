@@ -406,3 +406,27 @@ def test_topk_paths_identical(model, stage1):
                     out.append(e.topk())
             assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][2], out[1][2])
         check_exact(ds, model, k=10, stage1=stage1)
+
+
+def test_staged_dense_copy_equals_direct():
+    """mr_copy_dense stages copies of >= 8 MiB into pageable memory through
+    pinned buffers (chunked, host threads copy out); a pinned destination
+    goes straight through the DMA engine. Both give the same bytes, and the
+    group's pitched row copy (2 song shards) too."""
+    import torch
+
+    from musicrecommendation_amd.group import Group
+
+    ds = synth.generate(2000, 300, 21, alpha=0.87).dataset()  # 300 x ~12k songs x 8 B > 8 MiB
+    with Engine(ds, out_dtype="f64", topk=10) as e:
+        e.run("ibm")
+        staged = e.dense()
+        assert staged.nbytes >= 8 << 20
+        pinned = torch.empty((e.n_test, e.width), dtype=torch.float64, pin_memory=True)
+        _lib.check(e._L.mr_copy_dense(e._h, ctypes.c_void_p(pinned.data_ptr())), "mr_copy_dense")
+        assert np.array_equal(staged, pinned.numpy(), equal_nan=True)
+        exp, _, _ = native.fp_model(ds, "ibm", user_lo=0, user_hi=5)
+        assert np.array_equal(staged[:5], exp, equal_nan=True)
+    with Group(ds, song_shards=2, out_dtype="f64", topk=10) as g:
+        g.run("ibm")
+        assert np.array_equal(g.dense(), staged, equal_nan=True)
