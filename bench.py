@@ -278,6 +278,9 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
                          "traffic_source": "profiles/pmc_c5.json (rocprofv3 --pmc passes over one step, every "
                                            "engine kernel summed)" if traffic else None,
                          "traffic_GBps": traffic / step_s / 1e9 if traffic else None,
+                         # measured fabric bytes per second over the 8 TB/s peak: how saturated the
+                         # step is, whatever the byte model says (frac counts algorithmic bytes only)
+                         "traffic_frac": traffic / step_s / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "algorithmic_bytes_per_step": step_bytes},
             "threshold_mAP": maps,
             "mAP@10_lcm": evaluation.map_at_k(songs, full, 10) if world == 1 else None,
@@ -691,6 +694,9 @@ def main() -> None:
                 "traffic_source": traffic_src,
                 # measured fabric bytes over the same device time (traffic per launch ÷ avg_launch_us)
                 "traffic_GBps": traffic / (avg_us * 1e-6) / 1e9 if traffic else None,
+                # measured fetched + written bytes over the same device time, as a fraction of
+                # the 8 TB/s peak: the fabric saturation (frac counts algorithmic bytes only)
+                "traffic_frac": traffic / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS if traffic else None,
                 "algorithmic_bytes_per_launch": ab_dom,
                 "avg_launch_us": avg_us,
                 "launches_per_step": launches_per_step,

@@ -991,7 +991,9 @@ struct ScoreParams {
   const int2* te_rng;            // fused shape: per te_songs entry, (trs_off[s2], c_tr(s2))
   const long long* te_q;         // fused shape: per te_songs entry, q_song[s2]
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
-  const unsigned* lbits;         // fused, n_tr <= kBitmapMaxTrain: listener bitmap [n_s][lwords] (bit v = train user v)
+  const unsigned* tebits;        // fused, n_tr <= kBitmapMaxTrain: the listener bitmaps of every test user's
+                                 //   songs, user u's block at te_off[u] * lwords, word w of its j-th song at
+                                 //   + w * |T(u)| + j (bit v = train user v)
   int lwords;                    // words per bitmap row (0: stage 1 walks the listener lists)
   // fused stage 1 inputs
   const long long* trs_off;
@@ -1019,11 +1021,12 @@ struct ScoreParams {
   int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
 };
 
-// Fused stage 1 over listener bitmaps (mr_load builds lbits for train sets of
+// Fused stage 1 over listener bitmaps (mr_load builds tebits for train sets of
 // <= kBitmapMaxTrain users): Y[v] = sum over s2 in T(u) of q(s2) * [v in
 // L_tr(s2)] (ibm) or the count of s2 (ubm, then the fixed-point cosine,
-// MR:142-148). T(u)'s rows are staged word-major in LDS, kBitmapSongs songs
-// per batch (coalesced loads); thread t owns train users t + 256 r, keeps
+// MR:142-148). T(u)'s rows (precomputed per test user, word-major) are staged
+// in LDS kBitmapSongs songs per batch, one level of coalesced loads; thread t
+// owns train users t + 256 r, keeps
 // their sums in registers and adds each song's weight by bit test: no list
 // walk, no per-entry search, no atomics. The same integers as the walk
 // (order-free sums). Ends with a barrier; every Y[v] is written.
@@ -1039,11 +1042,24 @@ __device__ __forceinline__ void bitmap_stage1(const ScoreParams& p, unsigned lon
   unsigned long long ya[UPT];
 #pragma unroll
   for (int r = 0; r < UPT; ++r) ya[r] = 0ull;
+  const int nT = (int)(t1 - t0);
+  const unsigned* rows = p.tebits + (size_t)t0 * W;  // this user's block, word-major
   for (long long base = t0; base < t1; base += kBitmapSongs) {
     const int nb = (int)min((long long)kBitmapSongs, t1 - base);
-    for (int idx = tid; idx < nb * W; idx += kThreads) {  // row-major reads, word-major LDS
-      const int j = idx / W, w = idx - j * W;
-      bm[w * kBitmapSongs + j] = p.lbits[(size_t)p.te_songs[base + j] * W + w];
+    const int jb = (int)(base - t0);
+    {  // one level of independent coalesced loads: thread (half h, slot j) takes words 2i + h of song j
+      const int j = tid & (kBitmapSongs - 1), h = tid >> 7;
+      unsigned x[kBitmapMaxTrain / 64];
+#pragma unroll
+      for (int i = 0; i < kBitmapMaxTrain / 64; ++i) {
+        const int w = 2 * i + h;
+        x[i] = (w < W && j < nb) ? rows[(size_t)w * nT + jb + j] : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < kBitmapMaxTrain / 64; ++i) {
+        const int w = 2 * i + h;
+        if (w < W) bm[w * kBitmapSongs + j] = x[i];
+      }
     }
     for (int j = tid; j < kBitmapSongs; j += kThreads) {  // pad to whole groups of 4: weight 0
       long long q = 0;
@@ -1055,22 +1071,39 @@ __device__ __forceinline__ void bitmap_stage1(const ScoreParams& p, unsigned lon
       bq[j] = q;
     }
     __syncthreads();
-    const int ng = (nb + 3) >> 2;
-    for (int g = 0; g < ng; ++g) {
-      const ulonglong2 qa = *reinterpret_cast<const ulonglong2*>(bq + 4 * g);
-      const ulonglong2 qb = *reinterpret_cast<const ulonglong2*>(bq + 4 * g + 2);
+    // Groups of 4 songs, 8 groups per step with every LDS read issued before
+    // the arithmetic (one wave per SIMD: nothing else hides the LDS latency).
+    // Songs past nb have weight 0 (bq is zero-padded to the whole batch).
+    constexpr int GB = 8;
+    const int ng = (((nb + 3) >> 2) + GB - 1) / GB * GB;  // <= kBitmapSongs / 4
+    for (int g0 = 0; g0 < ng; g0 += GB) {
+      ulonglong2 qa[GB], qb[GB];
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        qa[i] = *reinterpret_cast<const ulonglong2*>(bq + 4 * (g0 + i));
+        qb[i] = *reinterpret_cast<const ulonglong2*>(bq + 4 * (g0 + i) + 2);
+      }
 #pragma unroll
       for (int r = 0; r < UPT; ++r) {
         if (r * kThreads >= n_tr) break;  // block-uniform
         const int v = tid + r * kThreads;
-        // lanes past n_tr read a valid word (row padding) and drop the sum below
-        const uint4 w4 = *reinterpret_cast<const uint4*>(bm + (min(v, n_tr - 1) >> 5) * kBitmapSongs + 4 * g);
+        // lanes past n_tr read a valid row word and drop the sum below
+        const unsigned* col = bm + (min(v, n_tr - 1) >> 5) * kBitmapSongs + 4 * g0;
+        uint4 w4[GB];
+#pragma unroll
+        for (int i = 0; i < GB; ++i) w4[i] = *reinterpret_cast<const uint4*>(col + 4 * i);
         const int sh = v & 31;
-        const unsigned long long m0 = (unsigned long long)(long long)__builtin_amdgcn_sbfe((int)w4.x, sh, 1);
-        const unsigned long long m1 = (unsigned long long)(long long)__builtin_amdgcn_sbfe((int)w4.y, sh, 1);
-        const unsigned long long m2 = (unsigned long long)(long long)__builtin_amdgcn_sbfe((int)w4.z, sh, 1);
-        const unsigned long long m3 = (unsigned long long)(long long)__builtin_amdgcn_sbfe((int)w4.w, sh, 1);
-        ya[r] += ((qa.x & m0) + (qa.y & m1)) + ((qb.x & m2) + (qb.y & m3));
+        unsigned long long sum = 0ull;
+#pragma unroll
+        for (int i = 0; i < GB; ++i) {
+          // sbfe yields 0 or 0xffffffff as an unsigned int: sign-extend it to 64 bits
+          const unsigned long long m0 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].x, sh, 1);
+          const unsigned long long m1 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].y, sh, 1);
+          const unsigned long long m2 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].z, sh, 1);
+          const unsigned long long m3 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].w, sh, 1);
+          sum += ((qa[i].x & m0) + (qa[i].y & m1)) + ((qb[i].x & m2) + (qb[i].y & m3));
+        }
+        ya[r] += sum;
       }
     }
     __syncthreads();  // the next batch overwrites the rows
@@ -2070,7 +2103,7 @@ struct mr_ctx {
   DevBuf<unsigned> tpack;  // fused shape: tile entries as (train user << 16) | tile-local song
   DevBuf<int2> te_rng;     // fused shape: listener range of every test-visible song
   DevBuf<long long> te_q;  // fused shape: its ibm weight q_song
-  DevBuf<unsigned> lbits;  // fused shape, n_tr <= kBitmapMaxTrain: listener bitmap [n_s][lwords]
+  DevBuf<unsigned> tebits;  // fused shape, n_tr <= kBitmapMaxTrain: T(u)'s listener bitmaps per test user
   int lwords = 0;
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
@@ -2104,7 +2137,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); lbits.release(); lwords = 0; te_songs.release(); trs_users.release(); toff.release(); sbound.release();
+    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); tebits.release(); lwords = 0; te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -2649,17 +2682,24 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     }
     if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
     if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
-    // Listener bitmaps of every song (bit v = new train user id v), for the
-    // bit-test stage 1 (bitmap_stage1) when the train set is small.
+    // Listener bitmaps (bit v = new train user id v) of every test user's
+    // songs, word-major per user, for the bit-test stage 1 (bitmap_stage1)
+    // when the train set is small: one level of coalesced loads per user.
     if (n_tr > 0 && n_tr <= kBitmapMaxTrain && c->opt.stage1_bitmap == 0) {
       const int W = (n_tr + 31) / 32;
-      std::vector<uint32_t> bits((size_t)n_s * W, 0u);
-      mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
-        for (int64_t s2 = a; s2 < b; ++s2)
-          for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1]; ++i)
-            bits[(size_t)s2 * W + (trs_users[i] >> 5)] |= 1u << (trs_users[i] & 31);
-      }, 4096);
-      if ((rc = dev_upload(c->lbits, bits.data(), bits.size(), st))) return rc;
+      std::vector<uint32_t> bits(std::max<size_t>(1, nte * W), 0u);
+      mr_par::parallel_for(n_te, [&](int64_t a, int64_t b, int) {
+        for (int64_t u = a; u < b; ++u) {
+          const int64_t t0 = d->te_off[u], nT = d->te_off[u + 1] - t0;
+          uint32_t* blk = bits.data() + (size_t)t0 * W;
+          for (int64_t j = 0; j < nT; ++j) {
+            const int s2 = d->te_songs[t0 + j];
+            for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1]; ++i)
+              blk[(size_t)(trs_users[i] >> 5) * nT + j] |= 1u << (trs_users[i] & 31);
+          }
+        }
+      }, 64);
+      if ((rc = dev_upload(c->tebits, bits.data(), bits.size(), st))) return rc;
       c->lwords = W;
     }
   } else {
@@ -2836,7 +2876,7 @@ int run_model(mr_ctx* c, int model) {
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
       sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused shape (else null)
-      sp.lbits = c->lbits.p; sp.lwords = c->lwords;  // fused, small train sets (else 0)
+      sp.tebits = c->tebits.p; sp.lwords = c->lwords;  // fused, small train sets (else 0)
 #ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
       sp.te_rng = nullptr;
 #endif

@@ -25,8 +25,14 @@ run() {  # name limit cmd...
 }
 
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/gpu.txt" || true
+# targeted tests first: TESTK="expr" (pytest -k), e.g. after a kernel change
+case ",$STEPS," in *,testk,*) run pytest_k 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread -k "$TESTK" ;; esac
 case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread ;; esac
 case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
+# C2 headline only (no north_star / e2e / CPU baseline): kernel A/B loops
+case ",$STEPS," in *,quick,*) run bench_quick 300 python bench.py --no-north-star --no-e2e --no-cpu-baseline --steps 2000 --warmup 50 ;; esac
+# per-workgroup phase stamps of the scoring kernel (diagnostic build): STAMPS="c2 ibm 0 auto"
+case ",$STEPS," in *,stamps,*) run stamps 300 python scripts/stamps.py ${STAMPS:-c2 ibm 0 auto} ;; esac
 case ",$STEPS," in *,ingest,*) MR_INGEST_TRACE=1 MR_LOAD_TRACE=1 run ingest_c4 900 python -u scripts/ingest_probe.py --config c4 --load --reps 3 --out "$OUT/ingest_c4.json" ;; esac
 case ",$STEPS," in *,bench,*) run bench 600 python bench.py ;; esac
 case ",$STEPS," in *,prof,*)
