@@ -1,0 +1,64 @@
+"""C2 kernel A/B: device time per step of the fused C2 step (graph of K steps,
+HIP events on the engine stream, as bench.py), for engine options given as
+key=value pairs, several rounds interleaved so drift hits every variant alike.
+The library variant comes from MR_ENGINE_LIB (scripts/build_variant.py).
+
+    python scripts/c2_ab.py [--steps 2000] [--rounds 3] "label:stage1_bitmap=0" "label2:"
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402,F401
+
+from musicrecommendation_amd import synth  # noqa: E402
+from musicrecommendation_amd.engine import Engine  # noqa: E402
+
+
+def parse(spec):
+    label, _, kv = spec.partition(":")
+    opts = {}
+    for item in filter(None, kv.split(",")):
+        k, v = item.split("=")
+        opts[k] = {"0": False, "1": True}.get(v, v) if k in ("stage1_bitmap", "topk_lists") else (
+            int(v) if v.lstrip("-").isdigit() else v)
+    return label, opts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--model", default="ibm")
+    a = ap.parse_args()
+    ds = synth.config(a.config).dataset()
+    engines = []
+    for spec in a.variants:
+        label, opts = parse(spec)
+        e = Engine(ds, out_dtype="f32", topk=10, **opts)
+        e.graph_capture(a.model, a.steps)
+        e.graph_launch()
+        e.sync()
+        engines.append((label, e))
+    res = {label: [] for label, _ in engines}
+    for _ in range(a.rounds):
+        for label, e in engines:
+            e.timing_begin()
+            e.graph_launch()
+            _n, ms = e.timing_end()
+            res[label].append(ms / a.steps * 1e3)
+    out = {"lib": os.environ.get("MR_ENGINE_LIB", "prod"), "config": a.config, "model": a.model,
+           "us_per_step": {k: sorted(v) for k, v in res.items()}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

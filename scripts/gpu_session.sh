@@ -32,6 +32,14 @@ case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as
 # C2 headline only (no north_star / e2e / CPU baseline): kernel A/B loops
 case ",$STEPS," in *,quick,*) run bench_quick 300 python bench.py --no-north-star --no-e2e --no-cpu-baseline --steps 2000 --warmup 50 ;; esac
 # per-workgroup phase stamps of the scoring kernel (diagnostic build): STAMPS="c2 ibm 0 auto"
+# C2 kernel A/B over library variants (scripts/build_variant.py) and engine options
+# (space-separated label:key=value,... specs): VARIANTS="prod notile" OPTS="bitmap: walk:stage1_bitmap=0"
+case ",$STEPS," in *,ab,*)
+  for v in ${VARIANTS:-prod}; do
+    lib=$v; [ "$v" = prod ] && lib=""
+    MR_ENGINE_LIB=$lib run ab_$v 300 python scripts/c2_ab.py ${OPTS:-base:}
+  done ;;
+esac
 case ",$STEPS," in *,stamps,*) run stamps 300 python scripts/stamps.py ${STAMPS:-c2 ibm 0 auto} ;; esac
 case ",$STEPS," in *,ingest,*) MR_INGEST_TRACE=1 MR_LOAD_TRACE=1 run ingest_c4 900 python -u scripts/ingest_probe.py --config c4 --load --reps 3 --out "$OUT/ingest_c4.json" ;; esac
 case ",$STEPS," in *,bench,*) run bench 600 python bench.py ;; esac
