@@ -123,10 +123,7 @@ typedef struct mr_options {
   int32_t topk_lists;  /* 1 = tile top-k of the wide shape by per-thread running lists only
                           (diagnostic); 0 (default) = a threshold pass first (about k candidates),
                           the lists only when ties overflow it. Results are identical. */
-  int32_t stage1_bitmap;/* fused shape, n_train_users <= 1024: 0 (default) = stage 1 by bit tests on
-                          per-song listener bitmaps (one 32-bit word per 32 train users), 1 = by
-                          the listener-list walk (A/B and tests). Results are identical. */
-  int32_t reserved[2];
+  int32_t reserved[3];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;

@@ -78,8 +78,7 @@ class MrOptions(ctypes.Structure):
         ("stage1_chunk", c_int32),
         ("train_order", c_int32),
         ("topk_lists", c_int32),
-        ("stage1_bitmap", c_int32),
-        ("reserved", c_int32 * 2),
+        ("reserved", c_int32 * 3),
     ]
 
 

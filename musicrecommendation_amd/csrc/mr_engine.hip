@@ -108,15 +108,8 @@ namespace {
 // LDS layout of k_score (bytes; every region 16-byte aligned).
 // ---------------------------------------------------------------------------
 struct ScoreLds {
-  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, gm, bm, bq, stage_lists, total;
+  int acc, y, heard, s_lo, s_w, s_pre, s_scan, wk, ws, fk, fs, flag, cpre, stg, gm, stage_lists, total;
 };
-
-// Fused stage 1 over listener bitmaps (train sets of <= kBitmapMaxTrain users,
-// e.g. C2's 500): per test user, the 32-bit words of T(u)'s listener rows are
-// staged in LDS kBitmapSongs songs at a time, word-major, and each thread adds
-// q(s2) into the register sums of its own train users by bit test.
-constexpr int kBitmapMaxTrain = 1024;  // <= 4 train users per thread, rows of <= 32 words
-constexpr int kBitmapSongs = 128;      // songs of T(u) per LDS batch
 // threshold top-k scratch of a 256-thread block with up to 64 rows
 // (= topk_scratch_bytes<kThreads, 64>())
 constexpr int kTopkScratch256 = (64 + 1) * 12 + 4 + 64 * 4 + 256 * 4;
@@ -134,8 +127,7 @@ __host__ __device__ inline int merge_lists_per_pass(int k);
 // candidate lists for the in-launch merge (stage_lists lists per pass), and
 // by the wide-tile top-k for its per-thread lists. n_chunks: separate shape's
 // stage-1 chunk count (prefix of the per-chunk neighbour counts).
-__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles, int n_chunks = 0,
-                                              int lwords = 0) {
+__host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int n_tiles, int n_chunks = 0) {
   ScoreLds L;
   const int fused = fused_ntr > 0 ? 1 : 0;
   const int kk = k > 0 ? k : 1;
@@ -160,8 +152,6 @@ __host__ __device__ inline ScoreLds score_lds(int bs, int fused_ntr, int k, int 
   L.cpre = o; o = align16(o + (n_chunks > 0 ? (n_chunks + 1) * 4 : 0));
   L.stg = o; o = align16(o + (n_chunks > 0 ? kWaves * kStgBytes : 0));
   L.gm = o; o = align16(o + kTopkScratch256);
-  L.bm = o; o = align16(o + lwords * kBitmapSongs * 4);   // [lwords][kBitmapSongs] row words
-  L.bq = o; o = align16(o + (lwords > 0 ? kBitmapSongs * 8 : 0));  // [kBitmapSongs] weights
   L.total = o;
   return L;
 }
@@ -991,10 +981,6 @@ struct ScoreParams {
   const int2* te_rng;            // fused shape: per te_songs entry, (trs_off[s2], c_tr(s2))
   const long long* te_q;         // fused shape: per te_songs entry, q_song[s2]
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
-  const unsigned* tebits;        // fused, n_tr <= kBitmapMaxTrain: the listener bitmaps of every test user's
-                                 //   songs, user u's block at te_off[u] * lwords, word w of its j-th song at
-                                 //   + w * |T(u)| + j (bit v = train user v)
-  int lwords;                    // words per bitmap row (0: stage 1 walks the listener lists)
   // fused stage 1 inputs
   const long long* trs_off;
   const int* trs_users;
@@ -1021,111 +1007,11 @@ struct ScoreParams {
   int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
 };
 
-// Fused stage 1 over listener bitmaps (mr_load builds tebits for train sets of
-// <= kBitmapMaxTrain users): Y[v] = sum over s2 in T(u) of q(s2) * [v in
-// L_tr(s2)] (ibm) or the count of s2 (ubm, then the fixed-point cosine,
-// MR:142-148). T(u)'s rows (precomputed per test user, word-major) are staged
-// in LDS kBitmapSongs songs per batch, one level of coalesced loads; thread t
-// owns train users t + 256 r, keeps
-// their sums in registers and adds each song's weight by bit test: no list
-// walk, no per-entry search, no atomics. The same integers as the walk
-// (order-free sums). Ends with a barrier; every Y[v] is written.
-template <int MODEL>
-__device__ __forceinline__ void bitmap_stage1(const ScoreParams& p, unsigned long long* Y, unsigned* heard, int blo,
-                                              int bhi, long long t0, long long t1, const double (&str)[kFusedPre],
-                                              unsigned char* bm_raw, unsigned char* bq_raw, int u, double two_f) {
-  constexpr int UPT = kBitmapMaxTrain / kThreads;
-  static_assert(UPT <= kFusedPre, "sqrt_tr prefetch covers the bitmap users");
-  unsigned* bm = reinterpret_cast<unsigned*>(bm_raw);          // [W][kBitmapSongs]
-  long long* bq = reinterpret_cast<long long*>(bq_raw);        // [kBitmapSongs]
-  const int tid = threadIdx.x, W = p.lwords, n_tr = p.n_tr;
-  unsigned long long ya[UPT];
-#pragma unroll
-  for (int r = 0; r < UPT; ++r) ya[r] = 0ull;
-  const int nT = (int)(t1 - t0);
-  const unsigned* rows = p.tebits + (size_t)t0 * W;  // this user's block, word-major
-  for (long long base = t0; base < t1; base += kBitmapSongs) {
-    const int nb = (int)min((long long)kBitmapSongs, t1 - base);
-    const int jb = (int)(base - t0);
-    {  // one level of independent coalesced loads: thread (half h, slot j) takes words 2i + h of song j
-      const int j = tid & (kBitmapSongs - 1), h = tid >> 7;
-      unsigned x[kBitmapMaxTrain / 64];
-#pragma unroll
-      for (int i = 0; i < kBitmapMaxTrain / 64; ++i) {
-        const int w = 2 * i + h;
-        x[i] = (w < W && j < nb) ? rows[(size_t)w * nT + jb + j] : 0u;
-      }
-#pragma unroll
-      for (int i = 0; i < kBitmapMaxTrain / 64; ++i) {
-        const int w = 2 * i + h;
-        if (w < W) bm[w * kBitmapSongs + j] = x[i];
-      }
-    }
-    for (int j = tid; j < kBitmapSongs; j += kThreads) {  // pad to whole groups of 4: weight 0
-      long long q = 0;
-      if (j < nb) {
-        const int s2 = p.te_songs[base + j];
-        q = MODEL == MR_IBM ? p.te_q[base + j] : 1ll;
-        if (s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
-      }
-      bq[j] = q;
-    }
-    __syncthreads();
-    // Groups of 4 songs, 8 groups per step with every LDS read issued before
-    // the arithmetic (one wave per SIMD: nothing else hides the LDS latency).
-    // Songs past nb have weight 0 (bq is zero-padded to the whole batch).
-    constexpr int GB = 8;
-    const int ng = (((nb + 3) >> 2) + GB - 1) / GB * GB;  // <= kBitmapSongs / 4
-    for (int g0 = 0; g0 < ng; g0 += GB) {
-      ulonglong2 qa[GB], qb[GB];
-#pragma unroll
-      for (int i = 0; i < GB; ++i) {
-        qa[i] = *reinterpret_cast<const ulonglong2*>(bq + 4 * (g0 + i));
-        qb[i] = *reinterpret_cast<const ulonglong2*>(bq + 4 * (g0 + i) + 2);
-      }
-#pragma unroll
-      for (int r = 0; r < UPT; ++r) {
-        if (r * kThreads >= n_tr) break;  // block-uniform
-        const int v = tid + r * kThreads;
-        // lanes past n_tr read a valid row word and drop the sum below
-        const unsigned* col = bm + (min(v, n_tr - 1) >> 5) * kBitmapSongs + 4 * g0;
-        uint4 w4[GB];
-#pragma unroll
-        for (int i = 0; i < GB; ++i) w4[i] = *reinterpret_cast<const uint4*>(col + 4 * i);
-        const int sh = v & 31;
-        unsigned long long sum = 0ull;
-#pragma unroll
-        for (int i = 0; i < GB; ++i) {
-          // sbfe yields 0 or 0xffffffff as an unsigned int: sign-extend it to 64 bits
-          const unsigned long long m0 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].x, sh, 1);
-          const unsigned long long m1 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].y, sh, 1);
-          const unsigned long long m2 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].z, sh, 1);
-          const unsigned long long m3 = (unsigned long long)(long long)(int)__builtin_amdgcn_sbfe(w4[i].w, sh, 1);
-          sum += ((qa[i].x & m0) + (qa[i].y & m1)) + ((qb[i].x & m2) + (qb[i].y & m3));
-        }
-        ya[r] += sum;
-      }
-    }
-    __syncthreads();  // the next batch overwrites the rows
-  }
-  const double rs_u = MODEL == MR_UBM ? p.sqrt_te[u] : 0.0;
-#pragma unroll
-  for (int r = 0; r < UPT; ++r) {
-    const int v = tid + r * kThreads;
-    if (v < n_tr)
-      Y[v] = (MODEL == MR_IBM || ya[r] == 0ull)
-                 ? ya[r]
-                 : (unsigned long long)neighbour_weight<MODEL>(ya[r], rs_u, str[r], two_f);
-  }
-  __syncthreads();
-}
-
 template <int MODEL, typename OutT, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
-  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles, FUSED ? 0 : p.n_chunks,
-                               FUSED ? p.lwords : 0);
+  const ScoreLds L = score_lds(bs, FUSED ? p.n_tr : 0, p.topk, p.n_tiles, FUSED ? 0 : p.n_chunks);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem_raw + L.acc);
   unsigned* heard = reinterpret_cast<unsigned*>(smem_raw + L.heard);
   long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
@@ -1191,37 +1077,32 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       str[r] = (MODEL == MR_UBM && v < p.n_tr) ? p.sqrt_tr[v] : 1.0;
     }
     unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
-    if (p.lwords > 0) {
-      bitmap_stage1<MODEL>(p, Y, heard, blo, bhi, t0, t1, str, smem_raw + L.bm, smem_raw + L.bq, u, two_f);
-      MR_STAMP(1);
-    } else {
-      for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
-      __syncthreads();
-      accumulate_neighbours<MODEL>(Y, t0, t1, p.te_songs, p.trs_off, p.trs_users, p.q_song,
-                                   reinterpret_cast<long long*>(smem_raw + L.s_lo),
-                                   reinterpret_cast<long long*>(smem_raw + L.s_w),
-                                   reinterpret_cast<int*>(smem_raw + L.s_pre),
-                                   reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi, false, 0, 0,
-                                   nullptr, 0, 0, p.te_rng, p.te_q);
-      MR_STAMP(1);
-      if (MODEL == MR_UBM) {  // overlap counts -> fixed-point cosines (MR:142-148), in place
-        const double rs_u = p.sqrt_te[u];
-        for (int v = tid, r = 0; v < p.n_tr; v += kThreads, ++r) {
-          const unsigned long long y = Y[v];
-          if (y != 0ull) {
-            double sv;
-            if (r < kFusedPre) {  // static register index: no scratch spill
-              sv = str[0];
+    for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
+    __syncthreads();
+    accumulate_neighbours<MODEL>(Y, t0, t1, p.te_songs, p.trs_off, p.trs_users, p.q_song,
+                                 reinterpret_cast<long long*>(smem_raw + L.s_lo),
+                                 reinterpret_cast<long long*>(smem_raw + L.s_w),
+                                 reinterpret_cast<int*>(smem_raw + L.s_pre),
+                                 reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi, false, 0, 0,
+                                 nullptr, 0, 0, p.te_rng, p.te_q);
+    MR_STAMP(1);
+    if (MODEL == MR_UBM) {  // overlap counts -> fixed-point cosines (MR:142-148), in place
+      const double rs_u = p.sqrt_te[u];
+      for (int v = tid, r = 0; v < p.n_tr; v += kThreads, ++r) {
+        const unsigned long long y = Y[v];
+        if (y != 0ull) {
+          double sv;
+          if (r < kFusedPre) {  // static register index: no scratch spill
+            sv = str[0];
 #pragma unroll
-              for (int x = 1; x < kFusedPre; ++x) sv = r == x ? str[x] : sv;
-            } else {
-              sv = p.sqrt_tr[v];
-            }
-            Y[v] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, sv, two_f);
+            for (int x = 1; x < kFusedPre; ++x) sv = r == x ? str[x] : sv;
+          } else {
+            sv = p.sqrt_tr[v];
           }
+          Y[v] = (unsigned long long)neighbour_weight<MODEL>(y, rs_u, sv, two_f);
         }
-        __syncthreads();
       }
+      __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < kFusedPre; ++j) {
@@ -2120,8 +2001,6 @@ struct mr_ctx {
   DevBuf<unsigned> tpack;  // fused shape: tile entries as (train user << 16) | tile-local song
   DevBuf<int2> te_rng;     // fused shape: listener range of every test-visible song
   DevBuf<long long> te_q;  // fused shape: its ibm weight q_song
-  DevBuf<unsigned> tebits;  // fused shape, n_tr <= kBitmapMaxTrain: T(u)'s listener bitmaps per test user
-  int lwords = 0;
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
@@ -2154,7 +2033,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); tebits.release(); lwords = 0; te_songs.release(); trs_users.release(); toff.release(); sbound.release();
+    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -2422,8 +2301,6 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.stage1 < 0 || o.stage1 > 4 || o.stage1 == 3)
     return fail(MR_E_INVALID, "stage1 %d is not 0 (auto), 1 (fused), 2 (separate) or 4 (wide)", o.stage1);
   if (o.topk_lists != 0 && o.topk_lists != 1) return fail(MR_E_INVALID, "topk_lists %d not 0 or 1", o.topk_lists);
-  if (o.stage1_bitmap != 0 && o.stage1_bitmap != 1)
-    return fail(MR_E_INVALID, "stage1_bitmap %d not 0 or 1", o.stage1_bitmap);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
@@ -2699,26 +2576,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     }
     if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
     if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
-    // Listener bitmaps (bit v = new train user id v) of every test user's
-    // songs, word-major per user, for the bit-test stage 1 (bitmap_stage1)
-    // when the train set is small: one level of coalesced loads per user.
-    if (n_tr > 0 && n_tr <= kBitmapMaxTrain && c->opt.stage1_bitmap == 0) {
-      const int W = (n_tr + 31) / 32;
-      std::vector<uint32_t> bits(std::max<size_t>(1, nte * W), 0u);
-      mr_par::parallel_for(n_te, [&](int64_t a, int64_t b, int) {
-        for (int64_t u = a; u < b; ++u) {
-          const int64_t t0 = d->te_off[u], nT = d->te_off[u + 1] - t0;
-          uint32_t* blk = bits.data() + (size_t)t0 * W;
-          for (int64_t j = 0; j < nT; ++j) {
-            const int s2 = d->te_songs[t0 + j];
-            for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1]; ++i)
-              blk[(size_t)(trs_users[i] >> 5) * nT + j] |= 1u << (trs_users[i] & 31);
-          }
-        }
-      }, 64);
-      if ((rc = dev_upload(c->tebits, bits.data(), bits.size(), st))) return rc;
-      c->lwords = W;
-    }
   } else {
     if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
@@ -2749,7 +2606,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
   c->score_lds = wide ? c->wide_lds
-                      : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks, c->lwords).total;
+                      : (size_t)score_lds(bs, fused ? n_tr : 0, k, n_tiles, fused ? 0 : n_chunks).total;
   if (c->score_lds > 160 * 1024)
     return fail(MR_E_INVALID, "scoring kernel needs %zu B of LDS (> 160 KiB): lower block_songs or topk",
                 c->score_lds);
@@ -2893,7 +2750,6 @@ int run_model(mr_ctx* c, int model) {
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
       sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused shape (else null)
-      sp.tebits = c->tebits.p; sp.lwords = c->lwords;  // fused, small train sets (else 0)
 #ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
       sp.te_rng = nullptr;
 #endif

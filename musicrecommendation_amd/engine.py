@@ -29,8 +29,7 @@ class Engine:
     def __init__(self, dataset: Dataset, *, device: int = 0, frac_bits: int = 32, song_lo: int = 0,
                  song_hi: int = 0, block_songs: int = 0, out_dtype: str = "f32", topk: int = 10,
                  dense: bool = True, time_kernels: bool = False, stage1: str = "auto",
-                 stage1_chunk: int = 0, train_order: str = "auto", topk_lists: bool = False,
-                 stage1_bitmap: bool = True):
+                 stage1_chunk: int = 0, train_order: str = "auto", topk_lists: bool = False):
         self._L = _lib.lib()
         opt = _lib.MrOptions()
         _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
@@ -47,7 +46,6 @@ class Engine:
         opt.stage1_chunk = stage1_chunk
         opt.train_order = {"auto": 0, "given": 1}[train_order]
         opt.topk_lists = 1 if topk_lists else 0
-        opt.stage1_bitmap = 0 if stage1_bitmap else 1
         self.opt = opt
         self.dtype = np.float32 if out_dtype == "f32" else np.float64
         self._h = ctypes.c_void_p()

@@ -26,7 +26,7 @@ def parse(spec):
     opts = {}
     for item in filter(None, kv.split(",")):
         k, v = item.split("=")
-        opts[k] = {"0": False, "1": True}.get(v, v) if k in ("stage1_bitmap", "topk_lists") else (
+        opts[k] = {"0": False, "1": True}.get(v, v) if k in ("topk_lists",) else (
             int(v) if v.lstrip("-").isdigit() else v)
     return label, opts
 

@@ -430,36 +430,3 @@ def test_staged_dense_copy_equals_direct():
     with Group(ds, song_shards=2, out_dtype="f64", topk=10) as g:
         g.run("ibm")
         assert np.array_equal(g.dense(), staged, equal_nan=True)
-
-
-@pytest.mark.parametrize("model", MODELS)
-def test_bitmap_stage1_equals_walk_and_oracle(model):
-    """The fused shape's stage 1 by bit tests on listener bitmaps (train sets of
-    <= 1024 users, default) and by the listener-list walk (stage1_bitmap=False)
-    give the fixed-point oracle's integers: KATs, fixtures, C1, C2, train sets
-    of 1024 (32 full words) and 1000 users (a partial last word), test users
-    with more songs than one LDS batch (128), frac_bits 16 / 40, a song shard."""
-    K = kat()
-    cases = [dataset_from_lines(K["train"], K["test"], K["labels"]),
-             dataset_from_lines(K["dup"]["train"], K["dup"]["test"], K["dup"]["labels"]),
-             synth_fixture("tiny")[0], synth_fixture("small")[0],
-             synth.config("c1").dataset(), synth.config("c2").dataset(),
-             synth.generate(1024, 6, 31, alpha=0.87).dataset(), synth.generate(1000, 6, 32, alpha=0.87).dataset()]
-    long_train = [f"A\ts{i}\t1" for i in range(300)] + [f"B\ts{i}\t1" for i in range(0, 300, 3)]
-    cases.append(dataset_from_lines(long_train, [f"X\ts{i}\t1" for i in range(0, 280, 2)], ["X\ts1\t1"]))
-    for ds in cases:
-        with Engine(ds, topk=10) as e:
-            assert e.shape == "fused"
-        a, sa = check_exact(ds, model)
-        b, sb = check_exact(ds, model, stage1_bitmap=False)
-        assert np.array_equal(a, b, equal_nan=True) and np.array_equal(sa, sb)
-    c2 = synth.config("c2").dataset()
-    for fb in (16, 40):
-        check_exact(c2, model, frac_bits=fb)
-    check_exact(c2, model, song_lo=3000, song_hi=11000)
-    with pytest.raises(_lib.EngineError):
-        o = _lib.MrOptions()
-        _lib.check(_lib.lib().mr_options_default(ctypes.byref(o)), "defaults")
-        o.stage1_bitmap = 2
-        h = ctypes.c_void_p()
-        _lib.check(_lib.lib().mr_create(ctypes.byref(o), ctypes.byref(h)), "mr_create")
