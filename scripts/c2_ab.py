@@ -3,7 +3,7 @@ HIP events on the engine stream, as bench.py), for engine options given as
 key=value pairs, several rounds interleaved so drift hits every variant alike.
 The library variant comes from MR_ENGINE_LIB (scripts/build_variant.py).
 
-    python scripts/c2_ab.py [--steps 2000] [--rounds 3] "label:stage1_bitmap=0" "label2:"
+    python scripts/c2_ab.py [--steps 2000] [--rounds 3] "label:topk_lists=1" "label2:"
 """
 from __future__ import annotations
 
