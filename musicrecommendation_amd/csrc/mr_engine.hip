@@ -1296,13 +1296,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     tdst.sc1 = true;
   }
 #endif
-#ifdef MR_EXP_NO_TILE_TOPK  // timing experiment only (wrong lists): the tile's first k keys, unranked
-  if (tid < k) topk_dst_write(tdst, tid, (long long)acc[tid], blo + tid);
-  const bool direct = true;
-  if (false) {
-#else
   if (!p.topk_lists && k <= kThreads / 16) {
-#endif
 #ifdef MR_STAMPS
     long long* sbt = sb ? sb + 3 : nullptr;  // sub-phase stamps in slots 12-14
 #else
@@ -1311,9 +1305,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
     thr_done = block_topk_threshold<kThreads, decltype(get_key), MR_TILE_ROWS>(
         bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws, kWaves * kMaxTopK, fk, fs, sbt, tdst);
   }
-#ifndef MR_EXP_NO_TILE_TOPK
   const bool direct = thr_done && tdst.key;
-#endif
   if (thr_done) {
   } else if (bs <= kMaxTopkTile) {
     block_topk(bw, k, get_key, wk, ws, fk, fs);
@@ -1389,15 +1381,6 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
         rk = ld_sc1(&ck[tid]);
         rs = ld_sc1(&cs[tid]);
       }
-#ifdef MR_EXP_NO_MERGE  // timing experiment only (wrong lists): the first tile's list as the user's
-      if (tid < k) {
-        p.top_key[(size_t)u * k + tid] = rk;
-        p.top_song[(size_t)u * k + tid] = rs;
-        p.top_score[(size_t)u * k + tid] = __longlong_as_double(rk);
-      }
-      if (tid == 0) p.counter[u] = 0u;
-      return;
-#endif
       MR_STAMP(6);
       auto get_r = [&](int, long long& key, int& song) { key = rk; song = rs; };  // called for i = tid only
       TopkDst mdst;
