@@ -335,12 +335,14 @@ def end_to_end(ds, model: str, reps: int = 3):
             t4 = time.perf_counter()
             e.close()
             rows.append((t4 - t0, t1 - t0, t2 - t1, t3 - t2, t4 - t3))
+            d2h_bytes = int(dense.nbytes)
+            del dense, d2  # freed outside the timed region (munmap of the previous rep's array)
     rows.sort()
     tot, ing, load, run, d2h = rows[len(rows) // 2]
     return {"ms": tot * 1e3, "pairs_per_s": ds.n_pairs() / tot,
             "breakdown_ms": {"ingest_tsv": ing * 1e3, "mr_load_index_h2d": load * 1e3, "mr_run": run * 1e3,
                              "d2h_dense": d2h * 1e3},
-            "d2h_bytes": int(dense.nbytes),
+            "d2h_bytes": d2h_bytes, "d2h_GBps": d2h_bytes / d2h / 1e9,
             "note": "wall clock, one GPU: native TSV ingest + mr_load (host index build + H2D) + mr_run + "
                     "D2H of the dense fp32 model; median of 3 (value excludes all of this but the kernels)"}
 

@@ -26,21 +26,21 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <vector>
 
 #ifndef MR_TILE_ROWS
 #define MR_TILE_ROWS 32  // threshold rows of the fused tile top-k (C2: 17.9 us vs 18.3 at 16; 8 < k falls back, 26.6)
 #endif
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstring>
-#include <limits>
-#include <string>
-#include <vector>
-
-#include <atomic>
 
 #include "mr_engine.h"
 #include "mr_internal.h"
@@ -1991,7 +1991,6 @@ struct mr_ctx {
   DevBuf<long long> stamps;
   // Pinned staging of large D2H copies (d2h_staged): two buffers, lazily
   // allocated, kept for the context's life.
-  void* stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   // Kernel timing ring: 3 events per timed batch (before stage 1, before the
   // score kernel, after it), recorded without host synchronisation and
@@ -2327,7 +2326,6 @@ int mr_destroy(mr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->release_data();
   for (int i = 0; i < 2; ++i) {
-    if (c->stage[i]) (void)hipHostFree(c->stage[i]);
     if (c->stage_ev[i]) (void)hipEventDestroy(c->stage_ev[i]);
   }
   for (auto& ev : c->ring) if (ev) (void)hipEventDestroy(ev);
@@ -2774,7 +2772,23 @@ namespace mr_internal {
 // into pageable memory (a fresh numpy array) are staged through two pinned
 // 64 MiB buffers: chunk i+1 is in flight while the host threads copy chunk i
 // out — and take the destination's first-touch page faults in parallel
-// (hipMemcpy from pageable memory: 9.9 GB/s at C3, one thread).
+// (hipMemcpy from pageable memory: 9.9 GB/s at C3, one thread; staged: 47-51
+// GB/s into a fresh numpy array, profiles/r03/d2h_c3.json). The two pinned
+// buffers are one process-wide pool (portable pinned memory, allocated on first
+// use and kept for the process: pinning 128 MiB costs ~14 ms, which a fresh
+// engine per call would pay every time — 29 vs 50 GB/s); one staged copy runs
+// at a time (the host threads are the bottleneck anyway).
+namespace {
+struct StagePool {
+  std::mutex m;
+  void* buf[2] = {nullptr, nullptr};
+};
+StagePool& stage_pool() {
+  static StagePool* p = new StagePool;  // never destroyed: outlives the HIP runtime's teardown order
+  return *p;
+}
+}  // namespace
+
 int d2h_staged(mr_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch, size_t row_bytes, size_t rows) {
   const size_t total = row_bytes * rows;
   if (total == 0) return MR_OK;
@@ -2787,15 +2801,17 @@ int d2h_staged(mr_ctx* c, void* dst, size_t dpitch, const void* src, size_t spit
     MR_HIP(hipStreamSynchronize(c->stream));
     return MR_OK;
   }
+  StagePool& pool = stage_pool();
+  std::lock_guard<std::mutex> lock(pool.m);
   for (int i = 0; i < 2; ++i) {
-    if (!c->stage[i]) MR_HIP(hipHostMalloc(&c->stage[i], kStage, hipHostMallocDefault));
+    if (!pool.buf[i]) MR_HIP(hipHostMalloc(&pool.buf[i], kStage, hipHostMallocPortable));
     if (!c->stage_ev[i]) MR_HIP(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
   }
   const size_t per = kStage / row_bytes;  // rows per chunk
   const size_t n_chunks = (rows + per - 1) / per;
   auto enqueue = [&](size_t k) -> int {
     const size_t r0 = k * per, nr = std::min(per, rows - r0);
-    MR_HIP(hipMemcpy2DAsync(c->stage[k & 1], row_bytes, static_cast<const char*>(src) + r0 * spitch, spitch,
+    MR_HIP(hipMemcpy2DAsync(pool.buf[k & 1], row_bytes, static_cast<const char*>(src) + r0 * spitch, spitch,
                             row_bytes, nr, hipMemcpyDeviceToHost, c->stream));
     MR_HIP(hipEventRecord(c->stage_ev[k & 1], c->stream));
     return MR_OK;
@@ -2806,7 +2822,7 @@ int d2h_staged(mr_ctx* c, void* dst, size_t dpitch, const void* src, size_t spit
   for (size_t k = 0; k < n_chunks; ++k) {
     MR_HIP(hipEventSynchronize(c->stage_ev[k & 1]));
     const size_t r0 = k * per, nr = std::min(per, rows - r0);
-    const char* from = static_cast<const char*>(c->stage[k & 1]);
+    const char* from = static_cast<const char*>(pool.buf[k & 1]);
     char* to = static_cast<char*>(dst) + r0 * dpitch;
     if (dpitch == row_bytes) {
       mr_par::parallel_for((int64_t)(nr * row_bytes), [&](int64_t a, int64_t b, int) {
