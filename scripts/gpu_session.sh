@@ -63,6 +63,8 @@ case ",$STEPS," in *,profc3,*)
   export TMPDIR=/tmp
   run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o bench -- python3 "$ROOT/bench.py" --config c3 --no-cpu-baseline --steps 20 --warmup 3 ;;
 esac
+# C4 step with the wide kernel's stage-2 walk forced: WALK=dense|list
+case ",$STEPS," in *,c4walk,*) MR_WIDE_WALK=${WALK:-dense} run bench_c4_${WALK:-dense} 900 python -u bench.py --config c4 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 ;; esac
 case ",$STEPS," in *,profc4,*)
   export TMPDIR=/tmp
   run prof_c4 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 ;;
