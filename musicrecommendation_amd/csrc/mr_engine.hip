@@ -65,7 +65,6 @@ constexpr long long kKeyNone = -1;        // valid keys are bit patterns of doub
 constexpr int kMaxTopkTile = 1024;        // songs per tile for the register top-k (4 per lane)
 constexpr int kMaxTopkLarge = 16;         // k limit of the wide-tile top-k (per-thread running lists)
 constexpr int kFusedPre = 4;              // fused shape: tile entries per thread prefetched before stage 1
-constexpr int kWideWalkDefault = 0;       // wide-shape stage-2 walk (wide_walk_opt)
 constexpr int kWideMapDefault = 1;        // wide-shape block mapping (wide_map_opt)
 
 thread_local std::string g_err = "no error";
@@ -744,8 +743,6 @@ struct NbrParams {
   long long* nbr_q;          // [batch][cap]
   int* nbr_cnt;              // [batch][n_chunks]
   const int* sbound;         // [n_s][n_chunks+1]: first trs_users index of each chunk (n_chunks > 1)
-  unsigned long long* nbr_mask;  // wide dense walk: [batch][n_groups] neighbour bits of 64 train users
-  int n_groups;
 };
 
 // First index in the sorted trs_users[lo, hi) whose user is >= v.
@@ -954,7 +951,6 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
     const int i = i0 + lane;
     const unsigned long long y = i < we ? Y[i] : 0ull;
     const unsigned long long m = __ballot(y != 0ull);
-    if (p.nbr_mask && lane == 0) p.nbr_mask[(size_t)bu * p.n_groups + ((cv0 + i0) >> 6)] = m;
     if (y != 0ull) {
       const int pos = base + __popcll(m & below);
       const int v = cv0 + i;
@@ -1009,13 +1005,6 @@ struct ScoreParams {
   double* top_score;
   long long* stamps;             // diagnostic build: [grid][8] phase timestamps
   int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
-  // wide dense walk (dense_walk = 1): per tile, segment lengths of every train
-  // user (u16, rows of 64 users) and each 64-user group's first entry; the
-  // neighbour bits of each group from k_neighbours
-  int dense_walk, n_groups;
-  const unsigned short* tcnt;    // [n_tiles][n_groups * 64]
-  const int* gbase;              // [n_tiles][n_groups]
-  const unsigned long long* nbr_mask;  // [batch][n_groups]
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -1603,91 +1592,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   __syncthreads();
   MR_STAMP(1);
 
-  if (p.dense_walk) {
-    // stage 2, dense walk: the tile's train side streamed in train-user order,
-    // 64 users per wave step (their segment lengths coalesced, starts by a DPP
-    // scan from the group's first entry), neighbours picked by the group's
-    // mask word and their weights read by rank from the compacted list; the
-    // active lanes of successive steps are packed into full 64-lane batches
-    // by a forward permute (no LDS space), then visited like the list walk.
-    const unsigned long long* msk = p.nbr_mask + (size_t)bu * p.n_groups;
-    const unsigned short* cn = p.tcnt + (size_t)tile * p.n_groups * 64;
-    const int* gbs = p.gbase + (size_t)tile * p.n_groups;
-    const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-    const uint2* tw = reinterpret_cast<const uint2*>(p.tsongs);
-    constexpr int kSeg = MR_WIDE_SEG, kW = (kSeg + 3) / 4 + 1;
-    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    auto visit = [&](bool act, int s0, int len, int idx) {
-      if (!act) return;
-      const unsigned long long q = (unsigned long long)nq[idx];
-      const int s1 = s0 + len;
-      const int wb = s0 >> 2;
-      const int we = len > 0 ? (s1 + 3) >> 2 : wb;
-      const int so = s0 & 3;
-      uint2 sw[kW];
-#pragma unroll
-      for (int j = 0; j < kW; ++j) sw[j] = wb + j < we ? tw[wb + j] : make_uint2(0u, 0u);
-#pragma unroll
-      for (int j = 0; j < kSeg; ++j) {
-        if (s0 + j < s1) {
-          const int e = (j & 3) + so;
-          const uint2 wv = e >= 4 ? sw[(j >> 2) + 1] : sw[j >> 2];
-          const unsigned x = ((e & 3) < 2 ? wv.x : wv.y) >> ((e & 1) * 16);
-          atomicAdd(&acc[x & 0xffffu], q);
-        }
-      }
-      for (int x0 = s0 + kSeg; x0 < s1; x0 += kSeg) {
-        int st[kSeg];
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < s1 ? (int)p.tsongs[x0 + j] : -1;
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j)
-          if (st[j] >= 0) atomicAdd(&acc[st[j]], q);
-      }
-    };
-    int ps = 0, pl = 0, pi = 0, npend = 0;  // pending neighbours in lanes [0, npend)
-    const int gpc = p.n_chunks > 1 ? p.chunk >> 6 : p.n_groups;  // groups per stage-1 chunk
-    for (int c = 0; c < p.n_chunks; ++c) {
-      const int g0 = c * gpc, g1 = min(p.n_groups, g0 + gpc);
-      int carry = 0;  // neighbours of chunk c in the groups before sg
-      for (int sg = g0; sg < g1; sg += 64) {
-        const unsigned long long mw = sg + lane < g1 ? msk[sg + lane] : 0ull;
-        const int pc = __popcll(mw);
-        const int incl = wave_incl_scan(pc);
-        const int rbase = carry + incl - pc;  // rank of group sg + lane's first neighbour in chunk c's list
-        carry += __builtin_amdgcn_readlane(incl, 63);
-        const int ng = min(64, g1 - sg);
-        for (int j = w; j < ng; j += NW) {
-          const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)mw, j);
-          const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(mw >> 32), j);
-          const unsigned long long m = ((unsigned long long)hi << 32) | lo;
-          if (m == 0ull) continue;
-          const int g = sg + j;
-          const int len = cn[(size_t)g * 64 + lane];
-          const int start = gbs[g] + wave_incl_scan(len) - len;
-          const int pos = __popcll(m & below);
-          const int idx = c * p.chunk + __builtin_amdgcn_readlane(rbase, j) + pos;
-          const bool act = (m >> lane) & 1ull;
-          const int nact = __popcll(m);
-          // a permutation: active lanes to npend + pos, the others after them (mod 64)
-          const int dst = ((act ? npend + pos : npend + nact + (lane - pos)) & 63) << 2;
-          const int rs = __builtin_amdgcn_ds_permute(dst, start);
-          const int rl = __builtin_amdgcn_ds_permute(dst, len);
-          const int ri = __builtin_amdgcn_ds_permute(dst, idx);
-          if (npend + nact >= 64) {  // a full batch: the old pending lanes + the first new ones
-            const bool old = lane < npend;
-            visit(true, old ? ps : rs, old ? pl : rl, old ? pi : ri);
-            ps = rs; pl = rl; pi = ri;  // the wrapped remainder, lanes [0, npend + nact - 64)
-            npend += nact - 64;
-          } else {
-            if (lane >= npend && lane < npend + nact) { ps = rs; pl = rl; pi = ri; }
-            npend += nact;
-          }
-        }
-      }
-    }
-    visit(lane < npend, ps, pl, pi);
-  } else
   // stage 2: R neighbours per thread in flight; each segment's first kSeg
   // entries are loaded in the same batch, longer tails loop.
   {
@@ -2081,11 +1985,6 @@ struct mr_ctx {
   DevBuf<int2> te_rng;     // fused shape: listener range of every test-visible song
   DevBuf<long long> te_q;  // fused shape: its ibm weight q_song
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
-  // wide dense walk: per-tile segment lengths / group starts, neighbour masks
-  int dense_walk = 0, n_groups = 0;
-  DevBuf<unsigned short> tcnt;
-  DevBuf<int> gbase;
-  DevBuf<unsigned long long> nbr_mask;
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
   DevBuf<unsigned char> dense;
@@ -2123,7 +2022,6 @@ struct mr_ctx {
     dense.release();
     stamps.release();
     flag.release();
-    tcnt.release(); gbase.release(); nbr_mask.release();
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -2207,15 +2105,6 @@ int merge_rows_opt() {
 
 // Wide-shape block mapping (ScoreParams.xcd_remap): 1 = tiles of a user on
 // one XCD, 2 = one tile's users per XCD; MR_WIDE_MAP=1/2 overrides.
-// Wide-shape stage-2 walk: 0 = the compacted neighbour list (toff gathers),
-// 1 = dense walk over the tile's train side; MR_WIDE_WALK=list/dense overrides.
-int wide_walk_opt() {
-  const char* e = std::getenv("MR_WIDE_WALK");
-  if (e && !std::strcmp(e, "dense")) return 1;
-  if (e && !std::strcmp(e, "list")) return 0;
-  return kWideWalkDefault;
-}
-
 int wide_map_opt() {
   static const int m = [] {
     const char* e = std::getenv("MR_WIDE_MAP");
@@ -2673,30 +2562,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
   }
-  c->dense_walk = 0;
-  c->n_groups = (std::max(1, n_tr) + 63) / 64;
-  if (wide && wide_walk_opt() == 1 && (n_chunks == 1 || chunk % 64 == 0)) {
-    // Dense walk inputs: per tile, every train user's segment length (rows of
-    // 64 users, zero-padded) and each group's first entry, from toff.
-    const int ng = c->n_groups;
-    mr_par::buffer<uint16_t> tcnt((size_t)n_tiles * ng * 64);
-    mr_par::buffer<int32_t> gbase((size_t)n_tiles * ng);
-    mr_par::parallel_for((int64_t)n_tiles * ng, [&](int64_t a, int64_t b, int) {
-      for (int64_t x = a; x < b; ++x) {
-        const int64_t t = x / ng, g = x % ng;
-        gbase[x] = toff[(size_t)t * n_tr + g * 64];
-        for (int l = 0; l < 64; ++l) {
-          const int64_t v = g * 64 + l;
-          tcnt[x * 64 + l] =
-              v < n_tr ? (uint16_t)(toff[(size_t)t * n_tr + v + 1] - toff[(size_t)t * n_tr + v]) : (uint16_t)0;
-        }
-      }
-    }, 256);
-    if ((rc = dev_upload(c->tcnt, tcnt.data(), tcnt.size(), st))) return rc;
-    if ((rc = dev_upload(c->gbase, gbase.data(), gbase.size(), st))) return rc;
-    if ((rc = dev_alloc(c->nbr_mask, (size_t)batch * ng))) return rc;
-    c->dense_walk = 1;
-  }
   if (k > 0) {
     const size_t nc = (size_t)(wide ? batch : n_te) * n_tiles * k;
     if ((rc = dev_alloc(c->cand_key, nc))) return rc;
@@ -2835,12 +2700,9 @@ int run_model(mr_ctx* c, int model) {
       NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->chunk, c->n_chunks, c->te_off.p, c->te_songs.p,
                    c->trs_off.p, c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
                    c->nbr_cnt.p, c->n_chunks > 1 ? c->sbound.p : nullptr};
-      np.nbr_mask = c->dense_walk ? c->nbr_mask.p : nullptr;
-      np.n_groups = c->n_groups;
       for (int y0 = 0; y0 < nb; y0 += 65535) {
         NbrParams q = np;
         q.user0 = user0 + y0;
-        if (q.nbr_mask) q.nbr_mask += (size_t)y0 * c->n_groups;
         q.nbr_v += (size_t)y0 * c->cap;
         q.nbr_q += (size_t)y0 * c->cap;
         q.nbr_cnt += (size_t)y0 * c->n_chunks;
@@ -2883,10 +2745,6 @@ int run_model(mr_ctx* c, int model) {
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       sp.topk_lists = c->opt.topk_lists;
-      sp.dense_walk = wide && c->dense_walk;
-      sp.n_groups = c->n_groups;
-      sp.tcnt = c->tcnt.p; sp.gbase = c->gbase.p;
-      sp.nbr_mask = c->nbr_mask.p ? c->nbr_mask.p + (size_t)y0 * c->n_groups : nullptr;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
                          c->score_lds, st, sp);
       MR_HIP(hipGetLastError());

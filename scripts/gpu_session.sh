@@ -31,6 +31,16 @@ case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -u -m pytest tests -m gp
 case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
 # C2 headline only (no north_star / e2e / CPU baseline): kernel A/B loops
 case ",$STEPS," in *,quick,*) run bench_quick 300 python bench.py --no-north-star --no-e2e --no-cpu-baseline --steps 2000 --warmup 50 ;; esac
+# The driver's command (--steps 20 --warmup 5) with the K steps split into
+# graphs of G steps (0 = one graph): GSTEPS="0 10 5 4 2 1", 3 runs each
+case ",$STEPS," in *,k20,*)
+  for gs in ${GSTEPS:-0 10 5 4 2 1}; do
+    for rep in 1 2 3; do
+      run k20_g${gs}_$rep 300 python bench.py --steps 20 --warmup 5 --graph-steps $gs --no-north-star --no-e2e --no-cpu-baseline
+    done
+  done
+  run k20_nograph 300 python bench.py --steps 20 --warmup 5 --no-graph --no-north-star --no-e2e --no-cpu-baseline ;;
+esac
 # per-workgroup phase stamps of the scoring kernel (diagnostic build): STAMPS="c2 ibm 0 auto"
 # C2 kernel A/B over library variants (scripts/build_variant.py) and engine options
 # (space-separated label:key=value,... specs): VARIANTS="prod notile" OPTS="bitmap: walk:stage1_bitmap=0"
@@ -63,8 +73,14 @@ case ",$STEPS," in *,profc3,*)
   export TMPDIR=/tmp
   run prof_c3 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3" -o bench -- python3 "$ROOT/bench.py" --config c3 --no-cpu-baseline --steps 20 --warmup 3 ;;
 esac
-# C4 step with the wide kernel's stage-2 walk forced: WALK=dense|list
-case ",$STEPS," in *,c4walk,*) MR_WIDE_WALK=${WALK:-dense} run bench_c4_${WALK:-dense} 900 python -u bench.py --config c4 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 ;; esac
+# PMC of one C4 neighbour batch (scripts/c4_probe.py): fetched bytes, then
+# instruction / wave-cycle counters, each pass its own run
+case ",$STEPS," in *,pmcc4,*)
+  export TMPDIR=/tmp
+  run c4probe 600 python scripts/c4_probe.py
+  run pmc4_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc4_fetch" -o p -- python3 "$ROOT/scripts/c4_probe.py"
+  run pmc4_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d "$OUT/pmc4_sq" -o p -- python3 "$ROOT/scripts/c4_probe.py" ;;
+esac
 case ",$STEPS," in *,profc4,*)
   export TMPDIR=/tmp
   run prof_c4 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 ;;

@@ -127,26 +127,10 @@ def test_wide_shape_small_inputs(model, chunk, k):
         Engine(synth_fixture("tiny")[0], stage1="wide", topk=17)
 
 
-@pytest.mark.parametrize("chunk", [0, 64, 128, 7])
 @pytest.mark.parametrize("model", MODELS)
-def test_wide_dense_walk(model, chunk, monkeypatch):
-    """The wide kernel's dense walk (the tile's segment lengths streamed in
-    train-user order, neighbours from k_neighbours' mask words, permute-packed
-    batches): bit-identical to the oracle, one and many tiles and stage-1
-    chunks (chunk 7 is not a multiple of 64: the list walk runs instead)."""
-    monkeypatch.setenv("MR_WIDE_WALK", "dense")
-    for ds in (synth_fixture("small")[0], synth.config("c2", n_test=13).dataset()):
-        for block in (256, 2048, 16384):
-            for k in (1, 10, 16):
-                check_exact(ds, model, k=k, stage1="wide", stage1_chunk=chunk, block_songs=block)
-
-
-@pytest.mark.parametrize("walk", ["list", "dense"])
-@pytest.mark.parametrize("model", MODELS)
-def test_large_train_set_exact(model, walk, monkeypatch):
+def test_large_train_set_exact(model):
     """n_train > 16384: chunked stage 1 (4096 train users per LDS chunk),
     16384-song tiles, XCD-grouped tiles; every user exact vs the oracle."""
-    monkeypatch.setenv("MR_WIDE_WALK", walk)
     ds = synth.generate_bulk(40_000, 21, 4).dataset()
     with Engine(ds, out_dtype="f64", topk=10) as e:
         # the widest tile the LDS holds, balanced over the tiles
