@@ -481,7 +481,7 @@ def main() -> None:
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
-    ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "pull", "wide", "user"],
+    ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "wide"],
                     help="launch shape (default: the engine's choice)")
     ap.add_argument("--block-songs", type=int, default=0, help="songs per tile (default: the engine's choice)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
@@ -685,9 +685,7 @@ def main() -> None:
                 "bound": "hbm",
                 "kernel": {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
                            "separate": "k_neighbours + k_score (per step)",
-                           "pull": "k_stage1_columns + k_pull + k_topk_merge (per step)",
-                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)",
-                           "user": "k_score_user (stages 1+2+3, one workgroup per test user, one launch per step)"}[eng.shape],
+                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)"}[eng.shape],
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
