@@ -489,6 +489,9 @@ def main() -> None:
                          "(--no-graph: K stream launches)")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per captured graph (must divide --steps; 0 = all K in one graph)")
+    ap.add_argument("--stream-sync", action="store_true",
+                    help="close the timed region with engine-stream waits before torch.cuda.synchronize() "
+                         "(default: one device-wide synchronize, the window's event read afterwards)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -596,12 +599,18 @@ def main() -> None:
         for _ in range(args.steps):
             step()
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
-    n_launch, win_ms = eng.timing_end()
-    drain()
+    if args.stream_sync:  # wait on the engine stream(s) first, then the device
+        n_launch, win_ms = eng.timing_end()
+        drain()
+    else:  # the closing event recorded, one device-wide wait (covers every stream)
+        eng.timing_stop()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if not args.stream_sync:
+        n_launch, win_ms = eng.timing_end()  # the window's events are complete: reads only
+        drain()
     pairs_total_rank = rank_pairs(args.steps)  # pairs scored by this rank over the timed steps
     stats = torch.tensor([elapsed, pairs_total_rank], dtype=torch.float64, device="cuda")
     if world > 1:

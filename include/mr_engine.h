@@ -309,8 +309,12 @@ int mr_kernel_times(mr_ctx* ctx, int32_t which, int64_t* launches, double* total
 /* Timing window: mr_timing_begin records an event on the context stream,
  * mr_timing_end records a second one, waits for it and returns the device
  * time between them and the number of scoring-kernel launches issued in
- * between (no per-launch events: the window does not perturb the launches). */
+ * between (no per-launch events: the window does not perturb the launches).
+ * mr_timing_stop records the closing event without waiting (a caller that
+ * synchronises the device itself reads the window later with mr_timing_end,
+ * which then records nothing). */
 int mr_timing_begin(mr_ctx* ctx);
+int mr_timing_stop(mr_ctx* ctx);
 int mr_timing_end(mr_ctx* ctx, int64_t* launches, double* total_ms);
 
 /* Diagnostic builds only (libmr_engine_stamps.so, -DMR_STAMPS): copy the

@@ -148,6 +148,7 @@ SIGNATURES = {
     "mr_kernel_times": (c_int, [c_void_p, c_int32, POINTER(c_int64), POINTER(c_double), c_int32]),
     "mr_debug_stamps": (c_int, [c_void_p, c_void_p, c_int64]),
     "mr_timing_begin": (c_int, [c_void_p]),
+    "mr_timing_stop": (c_int, [c_void_p]),
     "mr_timing_end": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_double)]),
     "mr_stream": (c_void_p, [c_void_p]),
     "mr_run_into": (c_int, [c_void_p, c_int, c_void_p]),

@@ -2005,6 +2005,7 @@ struct mr_ctx {
   // number of mr_run calls, no per-launch events.
   hipEvent_t win[2] = {nullptr, nullptr};
   bool win_open = false;
+  bool win_stopped = false;  // mr_timing_stop recorded win[1]
   void* dense_override = nullptr;  // mr_run_into: caller's device buffer for this run's dense model
   hipGraph_t graph = nullptr;          // mr_graph_capture: n steps of mr_run
   hipGraphExec_t graph_exec = nullptr;
@@ -3067,7 +3068,17 @@ int mr_timing_begin(mr_ctx* c) {
   MR_HIP(hipSetDevice(c->opt.device));
   MR_HIP(hipEventRecord(c->win[0], c->stream));
   c->win_open = true;
+  c->win_stopped = false;
   c->win_launches = 0;
+  return MR_OK;
+}
+
+int mr_timing_stop(mr_ctx* c) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->win_open) return fail(MR_E_STATE, "mr_timing_stop without mr_timing_begin");
+  MR_HIP(hipSetDevice(c->opt.device));
+  if (!c->win_stopped) MR_HIP(hipEventRecord(c->win[1], c->stream));
+  c->win_stopped = true;
   return MR_OK;
 }
 
@@ -3075,7 +3086,8 @@ int mr_timing_end(mr_ctx* c, int64_t* launches, double* total_ms) {
   if (!c) return fail(MR_E_INVALID, "null context");
   if (!c->win_open) return fail(MR_E_STATE, "mr_timing_end without mr_timing_begin");
   MR_HIP(hipSetDevice(c->opt.device));
-  MR_HIP(hipEventRecord(c->win[1], c->stream));
+  if (!c->win_stopped) MR_HIP(hipEventRecord(c->win[1], c->stream));
+  c->win_stopped = false;
   MR_HIP(hipEventSynchronize(c->win[1]));
   float t = 0.f;
   MR_HIP(hipEventElapsedTime(&t, c->win[0], c->win[1]));

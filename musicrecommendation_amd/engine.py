@@ -241,6 +241,10 @@ class Engine:
         """Open a timing window (one event on the engine stream)."""
         _lib.check(self._L.mr_timing_begin(self._h), "mr_timing_begin")
 
+    def timing_stop(self) -> None:
+        """Record the window's closing event without waiting (read it with timing_end)."""
+        _lib.check(self._L.mr_timing_stop(self._h), "mr_timing_stop")
+
     def timing_end(self) -> Tuple[int, float]:
         """Close the window: (scoring-kernel launches, device ms) since timing_begin."""
         n = ctypes.c_int64()

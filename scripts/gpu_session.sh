@@ -41,6 +41,13 @@ case ",$STEPS," in *,k20,*)
   done
   run k20_nograph 300 python bench.py --steps 20 --warmup 5 --no-graph --no-north-star --no-e2e --no-cpu-baseline ;;
 esac
+# closing the timed region: one device-wide synchronize vs engine-stream waits first
+case ",$STEPS," in *,k20sync,*)
+  for rep in 1 2 3 4; do
+    run k20_dev_$rep 300 python bench.py --steps 20 --warmup 5 --no-north-star --no-e2e --no-cpu-baseline
+    run k20_stream_$rep 300 python bench.py --steps 20 --warmup 5 --stream-sync --no-north-star --no-e2e --no-cpu-baseline
+  done ;;
+esac
 # per-workgroup phase stamps of the scoring kernel (diagnostic build): STAMPS="c2 ibm 0 auto"
 # C2 kernel A/B over library variants (scripts/build_variant.py) and engine options
 # (space-separated label:key=value,... specs): VARIANTS="prod notile" OPTS="bitmap: walk:stage1_bitmap=0"

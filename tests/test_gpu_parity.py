@@ -430,3 +430,32 @@ def test_staged_dense_copy_equals_direct():
     with Group(ds, song_shards=2, out_dtype="f64", topk=10) as g:
         g.run("ibm")
         assert np.array_equal(g.dense(), staged, equal_nan=True)
+
+
+def test_timing_window():
+    """mr_timing_begin / _stop / _end: the window counts the scoring launches
+    issued in it and its device time; _stop records the closing event without
+    waiting, _end then only reads it."""
+    import torch
+
+    ds, _ = synth_fixture("small")
+    with Engine(ds) as e:
+        assert e.fused
+        e.run("ibm")
+        e.sync()
+        e.timing_begin()
+        e.run("ibm")
+        e.run("ubm")
+        n, ms = e.timing_end()
+        assert n == 2 and ms > 0.0
+        e.timing_begin()
+        e.run("ibm")
+        e.timing_stop()
+        e.timing_stop()  # idempotent
+        torch.cuda.synchronize()
+        n, ms = e.timing_end()
+        assert n == 1 and ms > 0.0
+        with pytest.raises(_lib.EngineError):
+            e.timing_end()  # no open window
+        with pytest.raises(_lib.EngineError):
+            e.timing_stop()
