@@ -8,18 +8,20 @@ score written to HBM as fp32) and stage 3 (top-10 per test user) — what the
 reference's getItemBasedModel computes (MusicRecommender.scala MR:222-261),
 plus the recommendation list.
 
-Multi-GPU (one process per GPU, torchrun) — the layout the driver's N>1 run
-measures is the default ``--shard users``: weak scaling over test-user blocks,
-rank r scores test users [10r, 10r+10) of a 500 x 10N dataset over all songs
-(an exact partition of the model's pairs; no data-path collective). C2 is
-launch-latency-bound (one 18 us kernel per step), so any exchange would only
-add latency there ("C2 is too small to scale"). ``--shard
-songs`` runs the north star's song-range layout (every rank scores 10N test
-users on its song range, then one RCCL all-gather of the top-k lists + the
-device merge), ``--shard 2d --song-groups G_s`` the 2-D product (G_s song
-shards x N/G_s user blocks, the all-gather inside each block) — the layouts
-for the full-scale configs (``--config c4`` / ``c5``: strong scaling over the
-fixed test set; DESIGN.md §6 has the Amdahl table).
+Multi-GPU (one process per GPU, torchrun): the headline ``value`` stays C2 at
+every N (default ``--shard users``: weak scaling over test-user blocks, rank r
+scores test users [10r, 10r+10) of a 500 x 10N dataset over all songs, an
+exact partition of the model's pairs, no data-path collective — C2 is one
+~12 us latency-bound launch, SURVEY.md §8e: "C2 is too small to scale"). The
+C2 line carries a nested ``north_star`` block at every N, including 1: C4
+(1M train / 10k test / 384,546 songs, top-10) in the north star's 2-D layout
+(sharding.ShardScorer: G_s song shards = 1 at N = 1, 2 at even N, x N/G_s
+test-user blocks; ONE RCCL all-gather of the packed top-k record blocks per
+step inside each block, merged on the device), strong scaling over the fixed
+test set: slowest-rank ms per step, exchange ms, all-gather bytes and the
+process-group sizes. ``--shard songs`` / ``--shard 2d
+--song-groups G_s`` run those layouts as the main line (``--config c4`` /
+``c5`` for the full-scale configs).
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the byte model.
 """
