@@ -48,6 +48,19 @@ case ",$STEPS," in *,k20sync,*)
     run k20_stream_$rep 300 python bench.py --steps 20 --warmup 5 --stream-sync --no-north-star --no-e2e --no-cpu-baseline
   done ;;
 esac
+# host wait mode of the runtime's synchronisations: ROC_ACTIVE_WAIT_TIMEOUT (us of
+# active polling before an interrupt wait), WAITS="unset 100 1000 10000"
+case ",$STEPS," in *,k20wait,*)
+  for wv in ${WAITS:-unset 100 1000 10000}; do
+    for rep in 1 2 3; do
+      if [ "$wv" = unset ]; then
+        run k20_w${wv}_$rep 300 python bench.py --steps 20 --warmup 5 --no-north-star --no-e2e --no-cpu-baseline
+      else
+        ROC_ACTIVE_WAIT_TIMEOUT=$wv run k20_w${wv}_$rep 300 python bench.py --steps 20 --warmup 5 --no-north-star --no-e2e --no-cpu-baseline
+      fi
+    done
+  done ;;
+esac
 # per-workgroup phase stamps of the scoring kernel (diagnostic build): STAMPS="c2 ibm 0 auto"
 # C2 kernel A/B over library variants (scripts/build_variant.py) and engine options
 # (space-separated label:key=value,... specs): VARIANTS="prod notile" OPTS="bitmap: walk:stage1_bitmap=0"
