@@ -95,16 +95,25 @@ def threshold_map(scores: np.ndarray, ds: Dataset, thresholds=THRESHOLDS) -> flo
 
 
 def map_at_k(top_songs: np.ndarray, ds: Dataset, k: int = 10) -> float:
-    """Build-defined mAP@k of per-user top-k lists (song -1 = empty slot)."""
-    total = 0.0
-    for u in range(ds.n_test):
-        labels = set(ds.lab_songs[ds.lab_off[u]:ds.lab_off[u + 1]].tolist())
-        hits = 0
-        ap = 0.0
-        for i, s in enumerate(top_songs[u, :k].tolist(), start=1):
-            if s >= 0 and s in labels:
-                hits += 1
-                ap += hits / i
-        denom = min(k, len(labels))
-        total += ap / denom if denom else 0.0
-    return total / ds.n_test if ds.n_test else 0.0
+    """Build-defined mAP@k of per-user top-k lists (song -1 = empty slot):
+    per test user, Σ_i hit_i · (hits up to i) / i over the first k slots,
+    divided by min(k, |distinct labels|); users without labels count 0.
+    Vectorised: membership of every (user, song) slot in the user's label set
+    by one binary search over the sorted (user, song) label keys."""
+    n_te = ds.n_test
+    if n_te == 0:
+        return 0.0
+    top = np.asarray(top_songs)[:, :k].astype(np.int64)
+    lab_off = np.asarray(ds.lab_off, dtype=np.int64)
+    lab = np.asarray(ds.lab_songs, dtype=np.int64)
+    m = int(max(int(lab.max()) if lab.size else 0, int(top.max()) if top.size else 0)) + 1
+    lab_user = np.repeat(np.arange(n_te, dtype=np.int64), np.diff(lab_off))
+    keys = np.unique(lab_user * m + lab)  # distinct labels per user (set semantics)
+    n_lab = np.bincount(keys // m, minlength=n_te)
+    q = np.arange(n_te, dtype=np.int64)[:, None] * m + np.maximum(top, 0)
+    pos = np.minimum(np.searchsorted(keys, q), max(keys.size - 1, 0))
+    hit = (top >= 0) & (keys.size > 0) & (keys[pos] == q) if keys.size else np.zeros_like(top, dtype=bool)
+    ranks = np.arange(1, top.shape[1] + 1, dtype=np.float64)
+    ap = (hit * (np.cumsum(hit, axis=1) / ranks)).sum(axis=1)
+    denom = np.minimum(k, n_lab)
+    return float(np.where(denom > 0, ap / np.maximum(denom, 1), 0.0).sum() / n_te)
