@@ -217,7 +217,7 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     a, b = user_blocks(full.n_test, gu)[rank // gs]
     lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu))[rank % gs]
     ds = full if gu == 1 else full.subset_test_users(a, b)
-    eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi)
+    eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi, ibm_route=args.ibm_route)
     ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),
                          pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs)
     maps = {}
@@ -367,7 +367,8 @@ def north_star(args, world: int, rank: int, local: int):
     gen_s = time.perf_counter() - t0
     gs = 1 if world == 1 else (2 if world % 2 == 0 else world)
     t0 = time.perf_counter()
-    scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32")
+    scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32",
+                         ibm_route=args.ibm_route)
     load_s = time.perf_counter() - t0
 
     def timed(fn, k):
@@ -486,6 +487,8 @@ def main() -> None:
     ap.add_argument("--stage1", default="auto", choices=["auto", "fused", "separate", "wide"],
                     help="launch shape (default: the engine's choice)")
     ap.add_argument("--block-songs", type=int, default=0, help="songs per tile (default: the engine's choice)")
+    ap.add_argument("--ibm-route", default="auto", choices=["auto", "two_hop", "cooc"],
+                    help="wide shape's ItemBasedModel route (mr_options.ibm_route)")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
                     help="users shard, small configs: replay the K timed steps as one captured HIP graph "
                          "(--no-graph: K stream launches)")
@@ -535,8 +538,8 @@ def main() -> None:
         full = synth.config(args.config, n_test=n_te * nb).dataset()
         blocks = [full.subset_test_users(b * n_te, (b + 1) * n_te)
                   for b in range(rank * args.inflight, (rank + 1) * args.inflight)]
-        engines = [Engine(b, device=local, out_dtype="f32", topk=10, stage1=args.stage1, block_songs=args.block_songs)
-                   for b in blocks]
+        engines = [Engine(b, device=local, out_dtype="f32", topk=10, stage1=args.stage1, block_songs=args.block_songs,
+                          ibm_route=args.ibm_route) for b in blocks]
         ds = blocks[0]
         eng = engines[0]
         pairs_per_engine = [b.n_pairs() for b in blocks]
@@ -562,7 +565,8 @@ def main() -> None:
         trip = synth.config(args.config, n_test=None if bulk else n_te * world)
         full = trip.dataset()
         scorer = ShardScorer(full, rank, world, local, song_groups=song_groups_for(args, world), topk=10,
-                             out_dtype="f32", dense=dense_out, stage1=args.stage1, block_songs=args.block_songs)
+                             out_dtype="f32", dense=dense_out, stage1=args.stage1, block_songs=args.block_songs,
+                             ibm_route=args.ibm_route)
         eng = scorer.engine
         ds = scorer.ds
         engines = [eng]

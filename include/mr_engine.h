@@ -123,7 +123,16 @@ typedef struct mr_options {
   int32_t topk_lists;  /* 1 = tile top-k of the wide shape by per-thread running lists only
                           (diagnostic); 0 (default) = a threshold pass first (about k candidates),
                           the lists only when ties overflow it. Results are identical. */
-  int32_t reserved[3];
+  int32_t ibm_route;   /* ItemBasedModel route of the wide shape (the cosine sum of MR:249-257):
+                          0 = auto (co-listening index when it applies), 1 = two-hop (per test user,
+                          the train neighbours' weights, then their songs), 2 = co-listening index:
+                          each run first counts, for every test-visible song s2 and every song s of
+                          the shard, the train users that heard both (C[s2][s] = |L_tr(s2) ∩ L_tr(s)|,
+                          the numerator of MR:232-235), then scores u as Σ_{s2∈T(u)} q(s2)·C[s2][s].
+                          The same integer sum as the two-hop route: results are identical. Route 2
+                          needs the wide shape, tiles <= 32768 songs and train listener counts
+                          < 131072 (else MR_E_INVALID; auto then falls back to route 1). */
+  int32_t reserved[2];
 } mr_options;
 
 typedef struct mr_ctx mr_ctx;
@@ -152,6 +161,12 @@ int mr_launch_info(const mr_ctx* ctx, int32_t* shape, int32_t* block_songs, int3
  * fit 8 GiB; = n_test_users for the other shapes) and the stage-1 chunking of
  * the train users (*n_chunks chunks of *chunk users). */
 int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_chunks);
+
+/* ItemBasedModel route chosen by mr_load (mr_options.ibm_route): *route = 1
+ * two-hop, 2 co-listening index; for route 2 the index's rows (distinct
+ * test-visible songs with train listeners) and the entries its pool can hold
+ * (a bound on the shard's non-zero counts; 4 B each). Any pointer may be NULL. */
+int mr_route_info(const mr_ctx* ctx, int32_t* route, int32_t* n_rows, int64_t* pool_entries);
 
 /* Host only, before any load: the song tile of the wide shape that a context
  * with these options would use for n_train_users x n_test_users (the widest

@@ -78,7 +78,8 @@ class MrOptions(ctypes.Structure):
         ("stage1_chunk", c_int32),
         ("train_order", c_int32),
         ("topk_lists", c_int32),
-        ("reserved", c_int32 * 3),
+        ("ibm_route", c_int32),
+        ("reserved", c_int32 * 2),
     ]
 
 
@@ -126,6 +127,7 @@ SIGNATURES = {
     "mr_shard_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_launch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "mr_route_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int64)]),
     "mr_shard_tile_songs": (c_int, [POINTER(MrOptions), c_int32, c_int32, POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),

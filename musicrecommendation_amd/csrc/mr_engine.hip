@@ -1005,6 +1005,12 @@ struct ScoreParams {
   double* top_score;
   long long* stamps;             // diagnostic build: [grid][8] phase timestamps
   int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
+  // co-listening route (wide shape, ibm; k_cooc_build's index)
+  int n_rows, nseg;              // index rows; segment descriptors per LDS pass
+  const int* te_row;             // per te_songs entry: its index row, -1 = no train listener
+  const long long* seg_off;      // [tile][row]: first pool entry of the row's tile segment
+  const int* seg_len;            // [tile][row]: its entries
+  const unsigned* pool;          // entries (tile-local song << kCoocCntBits) | C[s2][s]
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -1530,11 +1536,112 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
+#ifndef MR_COOC_U
+#define MR_COOC_U 8         // co-listening route: pool entries per thread in flight
+#endif
+#ifndef MR_COOC_R
+#define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
+#endif
+#ifndef MR_COOC_NT
+#define MR_COOC_NT 1024     // co-listening index build: threads per workgroup
+#endif
+// Co-listening index entries: (tile-local song << kCoocCntBits) | count, so
+// tiles <= 32768 songs and counts < 131072 (mr_load checks both).
+constexpr int kCoocCntBits = 17;
+constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
+constexpr int kCoocMaxTile = 1 << (32 - kCoocCntBits);
 
+
+// Stage 2 of the wide shape as a walk over a list of train users: entry k <
+// cnt of the list is (v, w) = load_list(k) (v = -1 past the end); every
+// tile-local song x of v's segment in this tile (tsongs[toff_t[v] ..
+// toff_t[v+1])) gets acc[x] += w by an LDS atomic. R entries per thread per
+// iteration. Used by the two-hop scoring (list = the test user's neighbours,
+// w = their int64 weights) and by the co-listening index build (list = one
+// song's train listeners, w = 1).
+template <int NT, int R, int kSeg, typename AccT, typename WT, typename LoadList>
+__device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& load_list, const int* toff_t,
+                                                const unsigned short* tsongs, AccT* acc) {
+  // Software pipeline over iterations: iteration i gathers its segments
+  // while the toff pairs of i+1 and the list entries of i+2 are in flight
+  // (one memory latency covers the three dependent levels).
+  auto load_offs = [&](const int (&v)[R], int (&a)[R], int (&b)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      a[r] = b[r] = 0;
+      if (v[r] >= 0) { a[r] = toff_t[v[r]]; b[r] = toff_t[v[r] + 1]; }
+    }
+  };
+  int v0[R], a0[R], b0[R], v1[R], a1[R], b1[R], v2[R];
+  WT q0[R], q1[R], q2[R];
+  load_list(tid, v0, q0);
+  load_offs(v0, a0, b0);
+  load_list(tid + R * NT, v1, q1);
+  for (int k0 = tid; k0 < cnt; k0 += R * NT) {
+#ifndef MR_WIDE_U16
+    // a segment's first kSeg entries as 8-B words (4 tile-local ids each)
+    // from the aligned word holding entry a0: kW loads instead of kSeg
+    // 2-B loads (C4 21.9 vs 22.9 ms per 704-user batch, C3 1.093 vs 1.141 ms
+    // per step; MR_WIDE_U16 builds the 2-B form, profiles/r02/c4/vec_seg_ab.txt)
+    constexpr int kW = (kSeg + 3) / 4 + 1;
+    const uint2* tw = reinterpret_cast<const uint2*>(tsongs);
+    uint2 sw[R][kW];
+    int so[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int wb = a0[r] >> 2;
+      const int we = b0[r] > a0[r] ? (b0[r] + 3) >> 2 : wb;
+      so[r] = a0[r] & 3;
+#pragma unroll
+      for (int j = 0; j < kW; ++j) sw[r][j] = wb + j < we ? tw[wb + j] : make_uint2(0u, 0u);
+    }
+#else
+    int sg[R][kSeg];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int j = 0; j < kSeg; ++j) sg[r][j] = a0[r] + j < b0[r] ? (int)tsongs[a0[r] + j] : -1;
+#endif
+    load_offs(v1, a1, b1);                 // iteration i+1
+    load_list(k0 + 2 * R * NT, v2, q2);    // iteration i+2
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#ifndef MR_WIDE_U16
+#pragma unroll
+      for (int j = 0; j < kSeg; ++j) {
+        if (a0[r] + j < b0[r]) {
+          const int e = (j & 3) + so[r];  // 0..6: word j/4 or the next one
+          const uint2 wv = e >= 4 ? sw[r][(j >> 2) + 1] : sw[r][j >> 2];
+          const unsigned x = ((e & 3) < 2 ? wv.x : wv.y) >> ((e & 1) * 16);
+          atomicAdd(&acc[x & 0xffffu], q0[r]);
+        }
+      }
+#else
+#pragma unroll
+      for (int j = 0; j < kSeg; ++j)
+        if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q0[r]);
+#endif
+      for (int x0 = a0[r] + kSeg; x0 < b0[r]; x0 += kSeg) {
+        int st[kSeg];
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b0[r] ? (int)tsongs[x0 + j] : -1;
+#pragma unroll
+        for (int j = 0; j < kSeg; ++j)
+          if (st[j] >= 0) atomicAdd(&acc[st[j]], q0[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      a0[r] = a1[r]; b0[r] = b1[r]; q0[r] = q1[r];
+      v1[r] = v2[r]; q1[r] = q2[r];
+    }
+  }
+  (void)v0;
+}
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
-template <int MODEL, typename OutT, int NT, int KS>
+template <int MODEL, typename OutT, int NT, int KS, bool COOC>
 __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -1580,24 +1687,79 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   }
   const int nch = p.n_chunks;
   int cnt = 0;
-  for (int c0 = 0; c0 < nch; c0 += NT) {
-    const int cc = c0 + tid;
-    const int x = cc < nch ? p.nbr_cnt[(size_t)bu * nch + cc] : 0;
-    int tot;
-    const int pre = block_excl_scan_nt<NT>(x, &tot, s_scan);
-    if (cc < nch) cpre[cc] = cnt + pre;
-    cnt += tot;
+  if constexpr (!COOC) {
+    for (int c0 = 0; c0 < nch; c0 += NT) {
+      const int cc = c0 + tid;
+      const int x = cc < nch ? p.nbr_cnt[(size_t)bu * nch + cc] : 0;
+      int tot;
+      const int pre = block_excl_scan_nt<NT>(x, &tot, s_scan);
+      if (cc < nch) cpre[cc] = cnt + pre;
+      cnt += tot;
+    }
+    if (tid == 0) cpre[nch] = cnt;
   }
-  if (tid == 0) cpre[nch] = cnt;
   __syncthreads();
   MR_STAMP(1);
 
+  if constexpr (COOC) {
+    // stage 2 from the co-listening index: acc[s] += q(s2) * C[s2][s] over
+    // the tile segments of u's index rows, walked as one flattened list
+    // (coalesced pool reads). Descriptors of up to nseg rows per pass live in
+    // the top-k scratch, which is free until the epilogue.
+    long long* m_off = reinterpret_cast<long long*>(smem_raw + L.wk);
+    unsigned long long* m_q = reinterpret_cast<unsigned long long*>(m_off + p.nseg);
+    int* m_pre = reinterpret_cast<int*>(m_q + p.nseg);
+    const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+    const int* slen = p.seg_len + (size_t)tile * p.n_rows;
+    const long long* soff = p.seg_off + (size_t)tile * p.n_rows;
+    for (long long c0 = t0; c0 < t1; c0 += p.nseg) {
+      const int ns = (int)min<long long>(p.nseg, t1 - c0);
+      int len = 0;
+      long long off = 0;
+      unsigned long long q = 0ull;
+      if (tid < ns) {
+        const int r = p.te_row[c0 + tid];
+        if (r >= 0) {
+          len = slen[r];
+          off = soff[r];
+          q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
+        }
+      }
+      int total;
+      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
+      if (tid < ns) { m_off[tid] = off - pre; m_q[tid] = q; m_pre[tid] = pre; }
+      if (tid == 0) m_pre[ns] = total;
+      __syncthreads();
+      constexpr int U = MR_COOC_U;
+      // the thread's current row: entries [cb, ce) at pool[co + e], weight cq
+      int cur = -1, ce = 0;
+      long long co = 0;
+      unsigned long long cq = 0ull;
+      for (int e0 = tid; e0 < total; e0 += U * NT) {
+        unsigned x[U];
+        unsigned long long wq[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          const int e = e0 + j * NT;
+          x[j] = 0u;
+          wq[j] = 0ull;
+          if (e < total) {
+            while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_off[cur]; cq = m_q[cur]; }
+            x[j] = p.pool[co + e];
+            wq[j] = cq;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+          if (wq[j]) atomicAdd(&acc[x[j] >> kCoocCntBits], (unsigned long long)(x[j] & kCoocCntMask) * wq[j]);
+      }
+      __syncthreads();  // the next pass rewrites the descriptors
+    }
+  } else {
   // stage 2: R neighbours per thread in flight; each segment's first kSeg
   // entries are loaded in the same batch, longer tails loop.
-  {
     const int* nv = p.nbr_v + (size_t)bu * p.cap;
     const long long* nq = p.nbr_q + (size_t)bu * p.cap;
-    const int* toff_t = p.toff + (size_t)tile * p.n_tr;
     constexpr int R = MR_WIDE_R, kSeg = MR_WIDE_SEG;
     int cur = 0;
     auto load_list = [&](int k0, int (&v)[R], unsigned long long (&q)[R]) {
@@ -1614,81 +1776,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     };
-    // Software pipeline over iterations: iteration i gathers its segments
-    // while the toff pairs of i+1 and the list entries of i+2 are in flight
-    // (one memory latency covers the three dependent levels).
-    auto load_offs = [&](const int (&v)[R], int (&a)[R], int (&b)[R]) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        a[r] = b[r] = 0;
-        if (v[r] >= 0) { a[r] = toff_t[v[r]]; b[r] = toff_t[v[r] + 1]; }
-      }
-    };
-    int v0[R], a0[R], b0[R], v1[R], a1[R], b1[R], v2[R];
-    unsigned long long q0[R], q1[R], q2[R];
-    load_list(tid, v0, q0);
-    load_offs(v0, a0, b0);
-    load_list(tid + R * NT, v1, q1);
-    for (int k0 = tid; k0 < cnt; k0 += R * NT) {
-#ifndef MR_WIDE_U16
-      // a segment's first kSeg entries as 8-B words (4 tile-local ids each)
-      // from the aligned word holding entry a0: kW loads instead of kSeg
-      // 2-B loads (C4 21.9 vs 22.9 ms per 704-user batch, C3 1.093 vs 1.141 ms
-      // per step; MR_WIDE_U16 builds the 2-B form, profiles/r02/c4/vec_seg_ab.txt)
-      constexpr int kW = (kSeg + 3) / 4 + 1;
-      const uint2* tw = reinterpret_cast<const uint2*>(p.tsongs);
-      uint2 sw[R][kW];
-      int so[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int wb = a0[r] >> 2;
-        const int we = b0[r] > a0[r] ? (b0[r] + 3) >> 2 : wb;
-        so[r] = a0[r] & 3;
-#pragma unroll
-        for (int j = 0; j < kW; ++j) sw[r][j] = wb + j < we ? tw[wb + j] : make_uint2(0u, 0u);
-      }
-#else
-      int sg[R][kSeg];
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j) sg[r][j] = a0[r] + j < b0[r] ? (int)p.tsongs[a0[r] + j] : -1;
-#endif
-      load_offs(v1, a1, b1);                 // iteration i+1
-      load_list(k0 + 2 * R * NT, v2, q2);    // iteration i+2
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-#ifndef MR_WIDE_U16
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j) {
-          if (a0[r] + j < b0[r]) {
-            const int e = (j & 3) + so[r];  // 0..6: word j/4 or the next one
-            const uint2 wv = e >= 4 ? sw[r][(j >> 2) + 1] : sw[r][j >> 2];
-            const unsigned x = ((e & 3) < 2 ? wv.x : wv.y) >> ((e & 1) * 16);
-            atomicAdd(&acc[x & 0xffffu], q0[r]);
-          }
-        }
-#else
-#pragma unroll
-        for (int j = 0; j < kSeg; ++j)
-          if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q0[r]);
-#endif
-        for (int x0 = a0[r] + kSeg; x0 < b0[r]; x0 += kSeg) {
-          int st[kSeg];
-#pragma unroll
-          for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b0[r] ? (int)p.tsongs[x0 + j] : -1;
-#pragma unroll
-          for (int j = 0; j < kSeg; ++j)
-            if (st[j] >= 0) atomicAdd(&acc[st[j]], q0[r]);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        a0[r] = a1[r]; b0[r] = b1[r]; q0[r] = q1[r];
-        v1[r] = v2[r]; q1[r] = q2[r];
-      }
-    }
-    (void)v0;
+    walk_tile_lists<NT, R, kSeg, unsigned long long, unsigned long long>(tid, cnt, load_list,
+                                                                         p.toff + (size_t)tile * p.n_tr, p.tsongs, acc);
   }
   __syncthreads();
   MR_STAMP(2);
@@ -1778,6 +1867,100 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   }
   MR_STAMP(5);
   (void)lane;
+}
+
+// ---------------------------------------------------------------------------
+// Co-listening index (ibm_route 2), built at the start of every ibm run: for
+// index row r (a test-visible song s2 = row_song[r] with train listeners) and
+// song tile t, the counts C[s2][s] = |L_tr(s2) ∩ L_tr(s)| (the distinct-user
+// numerator of MR:232-235) of every song s of the tile with C > 0, as packed
+// entries (tile-local s << kCoocCntBits) | C in song order. One workgroup per
+// (row, tile): u32 counters in LDS, the row's listeners walked over the
+// tile-major train CSR like the two-hop stage 2 (weight 1), then compacted by
+// wave ballots. The row's tiles reserve their segments from its pool range
+// (row_base[r], capacity = a bound on the row's non-zeros) with one atomic on
+// row_cur[r] each. Rows come sorted by listener count, heaviest first, and
+// blockIdx.x = row * n_tiles + tile, so the long walks start first.
+// ---------------------------------------------------------------------------
+struct CoocParams {
+  int n_tr, n_rows, n_tiles, block_songs, song_lo, song_hi;
+  const int* toff;               // tile-major train CSR (ScoreParams.toff / tsongs)
+  const unsigned short* tsongs;
+  const long long* trs_off;      // train song -> users CSR (renumbered users, ascending)
+  const int* trs_users;
+  const int* row_song;           // [n_rows]
+  const long long* row_base;     // [n_rows] first pool entry of the row
+  unsigned* row_cur;             // [n_rows] entries reserved so far (zeroed before the launch)
+  unsigned* pool;
+  long long* seg_off;            // [tile][row]
+  int* seg_len;                  // [tile][row]
+};
+
+__host__ __device__ inline int cooc_build_lds(int bs) { return align16(bs * 4) + 16 * 4 + 16; }
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
+  constexpr int NW = NT / 64;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int bs = p.block_songs;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(bs * 4));
+  long long* s_base = reinterpret_cast<long long*>(s_scan + 16);
+  const int r = blockIdx.x / p.n_tiles, tile = blockIdx.x - r * p.n_tiles;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int blo = p.song_lo + tile * bs;
+  const int bw = min(p.song_hi, blo + bs) - blo;
+  for (int i = tid; i < bw; i += NT) cnt[i] = 0u;
+  __syncthreads();
+  const int s2 = p.row_song[r];
+  const long long a = p.trs_off[s2];
+  const int n = (int)(p.trs_off[s2 + 1] - a);
+  const int* lst = p.trs_users + a;
+  constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
+  auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int k = k0 + j * NT;
+      v[j] = k < n ? lst[k] : -1;
+      q[j] = 1u;
+    }
+  };
+  walk_tile_lists<NT, R, kSeg, unsigned, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs, cnt);
+  __syncthreads();
+  // compaction: wave w owns songs [wb, we) (a multiple of 64 wide), counted by
+  // ballots, then written in song order at the wave's offset
+  const int q4 = (bw + NT - 1) / NT * 64;
+  const int wb = min(bw, w * q4), we = min(bw, wb + q4);
+  int nz = 0;
+  for (int i0 = wb; i0 < we; i0 += 64) {
+    const int i = i0 + lane;
+    nz += __popcll(__ballot(i < we && cnt[i] != 0u));
+  }
+  if (lane == 0) s_scan[w] = nz;
+  __syncthreads();
+  int base = 0, total = 0;
+#pragma unroll
+  for (int x = 0; x < NW; ++x) {
+    base += x < w ? s_scan[x] : 0;
+    total += s_scan[x];
+  }
+  if (tid == 0) {
+    const unsigned at = total ? atomicAdd(&p.row_cur[r], (unsigned)total) : 0u;
+    const long long off = p.row_base[r] + at;
+    p.seg_off[(size_t)tile * p.n_rows + r] = off;
+    p.seg_len[(size_t)tile * p.n_rows + r] = total;
+    s_base[0] = off;
+  }
+  __syncthreads();
+  unsigned* out = p.pool + s_base[0];
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int i0 = wb; i0 < we; i0 += 64) {
+    const int i = i0 + lane;
+    const unsigned c = i < we ? cnt[i] : 0u;
+    const unsigned long long m = __ballot(c != 0u);
+    if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
+    base += __popcll(m);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2012,6 +2195,15 @@ struct mr_ctx {
   int graph_steps = 0;
   DevBuf<unsigned> flag;           // mr_topk_dense_device: negative-score flag
   long long win_launches = 0;
+  // co-listening route (mr_options.ibm_route, k_cooc_build)
+  int ibm_route = 1;               // 1 two-hop, 2 co-listening index
+  int n_rows = 0, nseg = 0;
+  long long pool_cap = 0;
+  size_t cooc_lds = 0;
+  ScoreKernel cooc_kernel = nullptr;
+  DevBuf<int> row_song, te_row, seg_len;
+  DevBuf<long long> row_base, seg_off;
+  DevBuf<unsigned> row_cur, pool;
 
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
@@ -2023,6 +2215,9 @@ struct mr_ctx {
     dense.release();
     stamps.release();
     flag.release();
+    row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
+    row_cur.release(); pool.release();
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -2144,11 +2339,21 @@ void pick_kernels(mr_ctx* c) {
     c->score_kernel[MODEL] = f64 ? k_score<MODEL, double, false> : k_score<MODEL, float, false>;
   if (c->shape == kShapeWide) {
     if (c->opt.topk == 10)
-      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, 10>
-                                   : k_score_wide<MODEL, float, kWideThreads, 10>;
+      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, 10, false>
+                                   : k_score_wide<MODEL, float, kWideThreads, 10, false>;
     else
-      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, kMaxTopkLarge>
-                                   : k_score_wide<MODEL, float, kWideThreads, kMaxTopkLarge>;
+      c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, kMaxTopkLarge, false>
+                                   : k_score_wide<MODEL, float, kWideThreads, kMaxTopkLarge, false>;
+    if constexpr (MODEL == MR_IBM) {
+      if (c->ibm_route == 2) {
+        if (c->opt.topk == 10)
+          c->cooc_kernel = f64 ? k_score_wide<MR_IBM, double, kWideThreads, 10, true>
+                               : k_score_wide<MR_IBM, float, kWideThreads, 10, true>;
+        else
+          c->cooc_kernel = f64 ? k_score_wide<MR_IBM, double, kWideThreads, kMaxTopkLarge, true>
+                               : k_score_wide<MR_IBM, float, kWideThreads, kMaxTopkLarge, true>;
+      }
+    }
   }
   c->nbr_kernel[MODEL] = k_neighbours<MODEL>;
 }
@@ -2284,6 +2489,8 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   if (o.stage1 < 0 || o.stage1 > 4 || o.stage1 == 3)
     return fail(MR_E_INVALID, "stage1 %d is not 0 (auto), 1 (fused), 2 (separate) or 4 (wide)", o.stage1);
   if (o.topk_lists != 0 && o.topk_lists != 1) return fail(MR_E_INVALID, "topk_lists %d not 0 or 1", o.topk_lists);
+  if (o.ibm_route < 0 || o.ibm_route > 2)
+    return fail(MR_E_INVALID, "ibm_route %d is not 0 (auto), 1 (two-hop) or 2 (co-listening index)", o.ibm_route);
   if (!o.dense && o.topk == 0) return fail(MR_E_INVALID, "dense=0 and topk=0: nothing to compute");
   if (o.stage1_chunk < 0 || o.stage1_chunk > kMaxLdsTrainUsers)
     return fail(MR_E_INVALID, "stage1_chunk %d outside [0,%d]", o.stage1_chunk, kMaxLdsTrainUsers);
@@ -2515,6 +2722,70 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                           : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
                                                                       budget / ((size_t)cap * 12)));
 
+  // ItemBasedModel route (mr_options.ibm_route). The co-listening index has
+  // one row per distinct test-visible song with train listeners, heaviest
+  // first; row r's pool range holds at most min(width, Σ_{v ∈ L_tr(s2)}
+  // |S(v) ∩ shard|) entries (its non-zero counts over the shard's songs).
+  int route = 1;
+  std::vector<int32_t> row_song, te_row;
+  std::vector<int64_t> row_base;
+  int64_t pool_cap = 0;
+  {
+    const char* why = nullptr;
+    int32_t max_c = 0;
+    if (!wide) why = "the wide shape only";
+    else if (bs > kCoocMaxTile) why = "song tiles <= 32768";
+    if (!why && c->opt.ibm_route != 1) {
+      const int64_t nte = d->te_off[n_te];
+      std::vector<int32_t> row_of(n_s, -1);
+      for (int64_t i = 0; i < nte; ++i) {
+        const int s2 = d->te_songs[i];
+        if (col_tr[s2] > 0 && row_of[s2] < 0) { row_of[s2] = 0; row_song.push_back(s2); }
+      }
+      std::sort(row_song.begin(), row_song.end(), [&](int x, int y) {
+        return col_tr[x] != col_tr[y] ? col_tr[x] > col_tr[y] : x < y;
+      });
+      for (size_t r = 0; r < row_song.size(); ++r) {
+        row_of[row_song[r]] = (int32_t)r;
+        max_c = std::max(max_c, col_tr[row_song[r]]);
+      }
+      te_row.resize(std::max<int64_t>(1, nte));
+      for (int64_t i = 0; i < nte; ++i) te_row[i] = row_of[d->te_songs[i]];
+      if (max_c > (int32_t)kCoocCntMask) why = "train listener counts < 131072";
+      else if ((long long)row_song.size() * n_tiles > INT32_MAX) why = "rows x tiles < 2^31";
+    }
+    if (!why && c->opt.ibm_route != 1) {
+      // |S(v) ∩ [lo, hi)| of every (renumbered) train user, then the row bounds
+      std::vector<int32_t> deg((size_t)std::max(1, n_tr));
+      mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
+        for (int64_t v = a; v < b; ++v) {
+          const int32_t* r0 = tr_songs + tr_off[v];
+          const int32_t* r1 = tr_songs + tr_off[v + 1];
+          deg[v] = (int32_t)(std::lower_bound(r0, r1, hi) - std::lower_bound(r0, r1, lo));
+        }
+      });
+      const int64_t nr = (int64_t)row_song.size();
+      row_base.assign((size_t)nr + 1, 0);
+      mr_par::parallel_for(nr, [&](int64_t a, int64_t b, int) {
+        for (int64_t r = a; r < b; ++r) {
+          const int s2 = row_song[r];
+          int64_t sum = 0;
+          for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1] && sum < width; ++i) sum += deg[trs_users[i]];
+          row_base[r] = std::min<int64_t>(sum, width);
+        }
+      }, 256);
+      pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
+      row_base[nr] = pool_cap;
+      size_t free_b = 0, total_b = 0;
+      MR_HIP(hipMemGetInfo(&free_b, &total_b));
+      if ((double)pool_cap * 4.0 > 0.5 * (double)free_b) why = "a pool within half the free device memory";
+    }
+    if (c->opt.ibm_route == 2 && why)
+      return fail(MR_E_INVALID, "ibm_route 2 (co-listening index) needs %s", why);
+    route = (c->opt.ibm_route != 1 && !why) ? 2 : 1;
+    trace("route");
+  }
+
   hipStream_t st = c->stream;
   if ((rc = dev_upload(c->tr_off, reinterpret_cast<const long long*>(tr_off), (size_t)n_tr + 1, st))) return rc;
   if ((rc = dev_upload(c->te_off, reinterpret_cast<const long long*>(d->te_off), (size_t)n_te + 1, st))) return rc;
@@ -2563,8 +2834,21 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
     if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
   }
+  if (route == 2) {
+    const size_t nr = row_song.size();
+    if ((rc = dev_upload(c->row_song, row_song.data(), nr, st))) return rc;
+    if ((rc = dev_upload(c->te_row, te_row.data(), te_row.size(), st))) return rc;
+    if ((rc = dev_upload(c->row_base, reinterpret_cast<const long long*>(row_base.data()), nr + 1, st))) return rc;
+    if ((rc = dev_alloc(c->row_cur, nr))) return rc;
+    if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
+    if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
+    if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
+  }
   if (k > 0) {
-    const size_t nc = (size_t)(wide ? batch : n_te) * n_tiles * k;
+    // wide: per-tile candidates of one launch (a neighbour batch; the
+    // co-listening route launches up to 65528 users at once)
+    const int cand_users = !wide ? n_te : route == 2 ? std::max(batch, std::min(n_te, 65528)) : batch;
+    const size_t nc = (size_t)cand_users * n_tiles * k;
     if ((rc = dev_alloc(c->cand_key, nc))) return rc;
     if ((rc = dev_alloc(c->cand_song, nc))) return rc;
     // keys then songs in ONE record block: the send buffer of the song-shard
@@ -2584,6 +2868,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
 
   c->fused = fused;
   c->shape = shape;
+  c->ibm_route = route;
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
@@ -2598,6 +2883,19 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
+  }
+  if (route == 2) {
+    c->n_rows = (int)row_song.size();
+    c->pool_cap = pool_cap;
+    // the score kernel's row descriptors (20 B each) in its top-k scratch
+    const WideLds<kWideThreads> WL = wide_lds<kWideThreads>(bs, k, n_chunks);
+    c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 4) / 20);
+    if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
+    c->cooc_lds = (size_t)cooc_build_lds(bs);
+    MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->score_lds));
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->cooc_lds));
   }
   if (wide && k > 0) {
     c->merge_lds = (size_t)merge_lds_bytes(k);
@@ -2618,6 +2916,15 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->chunk = chunk; c->n_chunks = n_chunks;
   c->loaded = true;
   c->ran = false;
+  return MR_OK;
+}
+
+int mr_route_info(const mr_ctx* c, int32_t* route, int32_t* n_rows, int64_t* pool_entries) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_route_info before mr_load");
+  if (route) *route = c->ibm_route;
+  if (n_rows) *n_rows = c->n_rows;
+  if (pool_entries) *pool_entries = c->pool_cap;
   return MR_OK;
 }
 
@@ -2679,7 +2986,71 @@ int flush_timing(mr_ctx* c) {
   return MR_OK;
 }
 
+// The co-listening route of an ibm run: the index build (k_cooc_build, in
+// the stage-1 timing slot), then the scoring kernel over all test users (in
+// launches of <= 65528 users) and the per-user merge of the tile lists.
+int run_cooc(mr_ctx* c) {
+  hipStream_t st = c->stream;
+  const bool timed = c->opt.time_kernels != 0;
+  const int k = c->opt.topk;
+  hipEvent_t* ev = nullptr;
+  if (timed) {
+    if (c->ring_used == mr_ctx::kRing) {
+      int rc = flush_timing(c);
+      if (rc) return rc;
+    }
+    ev = &c->ring[(size_t)c->ring_used * 3];
+    c->ring_has_stage1[c->ring_used] = true;
+    c->ring_used++;
+    MR_HIP(hipEventRecord(ev[0], st));
+  }
+  if (c->n_rows > 0) {
+    MR_HIP(hipMemsetAsync(c->row_cur.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
+    CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
+                  c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
+                  c->seg_off.p, c->seg_len.p};
+    hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_rows * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
+    MR_HIP(hipGetLastError());
+  }
+  if (timed) MR_HIP(hipEventRecord(ev[1], st));
+  for (int y0 = 0; y0 < c->n_te; y0 += 65528) {
+    const int ny = std::min(65528, c->n_te - y0);
+    const int remap = wide_map_opt();
+    ScoreParams sp{};
+    sp.chunk = c->chunk; sp.n_chunks = c->n_chunks;
+    sp.n_users = ny; sp.xcd_remap = remap;
+    sp.merge_rows = merge_rows_opt();
+    sp.n_tr = c->n_tr;
+    sp.user0 = y0;
+    sp.song_lo = c->song_lo; sp.song_hi = c->song_hi; sp.width = c->width;
+    sp.block_songs = c->block_songs; sp.n_tiles = c->n_tiles;
+    sp.frac_bits = c->opt.frac_bits; sp.topk = k; sp.dense = c->opt.dense;
+    sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
+    sp.sqrt_c = c->sqrt_c.p; sp.q_song = c->q_song.p;
+    sp.n_rows = c->n_rows; sp.nseg = c->nseg;
+    sp.te_row = c->te_row.p; sp.seg_off = c->seg_off.p; sp.seg_len = c->seg_len.p; sp.pool = c->pool.p;
+    sp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p;
+    sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
+    sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
+    sp.stamps = nullptr;  // the stamps buffer is sized for one neighbour batch
+    sp.topk_lists = c->opt.topk_lists;
+    hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(kWideThreads), c->score_lds, st, sp);
+    MR_HIP(hipGetLastError());
+    if (k > 0 && c->n_tiles > 1) {
+      MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, (long long)k, c->cand_key.p,
+                     c->cand_song.p, c->top_key.p + (size_t)y0 * k, c->top_song.p + (size_t)y0 * k,
+                     c->top_score.p + (size_t)y0 * k};
+      hipLaunchKernelGGL(k_topk_merge, dim3(ny), dim3(kThreads), c->merge_lds, st, mp);
+      MR_HIP(hipGetLastError());
+    }
+    if (c->win_open) c->win_launches++;
+  }
+  if (timed) MR_HIP(hipEventRecord(ev[2], st));
+  return MR_OK;
+}
+
 int run_model(mr_ctx* c, int model) {
+  if (model == MR_IBM && c->ibm_route == 2) return run_cooc(c);
   hipStream_t st = c->stream;
   const bool timed = c->opt.time_kernels != 0;
   const int k = c->opt.topk;

@@ -16,6 +16,8 @@ from .dataset import Dataset
 
 MODELS = {"ubm": _lib.MR_UBM, "ibm": _lib.MR_IBM, _lib.MR_UBM: _lib.MR_UBM, _lib.MR_IBM: _lib.MR_IBM}
 KERNELS = {"neighbours": 0, "score": 1}
+# mr_options.ibm_route: the wide shape's ItemBasedModel route
+IBM_ROUTES = {"auto": 0, "two_hop": 1, "cooc": 2}
 
 
 def model_id(model: Union[str, int]) -> int:
@@ -29,7 +31,8 @@ class Engine:
     def __init__(self, dataset: Dataset, *, device: int = 0, frac_bits: int = 32, song_lo: int = 0,
                  song_hi: int = 0, block_songs: int = 0, out_dtype: str = "f32", topk: int = 10,
                  dense: bool = True, time_kernels: bool = False, stage1: str = "auto",
-                 stage1_chunk: int = 0, train_order: str = "auto", topk_lists: bool = False):
+                 stage1_chunk: int = 0, train_order: str = "auto", topk_lists: bool = False,
+                 ibm_route: str = "auto"):
         self._L = _lib.lib()
         opt = _lib.MrOptions()
         _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
@@ -46,6 +49,7 @@ class Engine:
         opt.stage1_chunk = stage1_chunk
         opt.train_order = {"auto": 0, "given": 1}[train_order]
         opt.topk_lists = 1 if topk_lists else 0
+        opt.ibm_route = IBM_ROUTES[ibm_route]
         self.opt = opt
         self.dtype = np.float32 if out_dtype == "f32" else np.float64
         self._h = ctypes.c_void_p()
@@ -72,6 +76,12 @@ class Engine:
         _lib.check(self._L.mr_batch_info(self._h, ctypes.byref(b), ctypes.byref(ch), ctypes.byref(nch)),
                    "mr_batch_info")
         self.batch, self.stage1_chunk, self.n_chunks = b.value, ch.value, nch.value
+        rt, nr, pe = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        _lib.check(self._L.mr_route_info(self._h, ctypes.byref(rt), ctypes.byref(nr), ctypes.byref(pe)),
+                   "mr_route_info")
+        # "two_hop" or "cooc" (co-listening index), and the index's size
+        self.ibm_route = {1: "two_hop", 2: "cooc"}[rt.value]
+        self.cooc_rows, self.cooc_pool_entries = nr.value, pe.value
 
     # ---- lifecycle ----------------------------------------------------------
     def close(self) -> None:

@@ -178,7 +178,7 @@ class ShardScorer:
 
     def __init__(self, ds: Dataset, rank: int, world: int, device: int, *, song_groups: Optional[int] = None,
                  topk: int = 10, dense: bool = True, out_dtype: str = "f32", time_kernels: bool = False,
-                 stage1: str = "auto", block_songs: int = 0):
+                 stage1: str = "auto", block_songs: int = 0, ibm_route: str = "auto"):
         import torch
         from .engine import Engine
 
@@ -193,7 +193,7 @@ class ShardScorer:
         self.group = block_group(rank, world, self.gs) if world > 1 else None
         self.engine = Engine(self.ds, device=device, song_lo=self.song_lo, song_hi=self.song_hi, topk=topk,
                              dense=dense, out_dtype=out_dtype, time_kernels=time_kernels, stage1=stage1,
-                             block_songs=block_songs)
+                             block_songs=block_songs, ibm_route=ibm_route)
         self.device = torch.device("cuda", device)
         n_te = self.ds.n_test
         # the exchange: this rank's lists as ONE record block (keys, then songs),

@@ -79,6 +79,16 @@ case ",$STEPS," in *,prof,*)
 esac
 case ",$STEPS," in *,c4,*) run bench_c4 900 python -u bench.py --config c4 --steps 5 --warmup 2 ;; esac
 case ",$STEPS," in *,c5,*) run bench_c5 900 python -u bench.py --config c5 --steps 3 --warmup 1 ;; esac
+# C4 per ItemBasedModel route (mr_options.ibm_route): ROUTES="cooc two_hop", kernels only
+case ",$STEPS," in *,c4route,*)
+  for r in ${ROUTES:-cooc two_hop}; do
+    run bench_c4_$r 900 python -u bench.py --config c4 --steps 5 --warmup 2 --no-e2e --no-cpu-baseline --no-north-star --ibm-route $r
+  done ;;
+esac
+case ",$STEPS," in *,profc4cooc,*)
+  export TMPDIR=/tmp
+  run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;
+esac
 # Rehearsal of the driver's N>1 command on one GPU (gloo, every rank on device 0;
 # the real runs use RCCL, one GPU per rank): the C2 line + its north_star block.
 for n in 2 4; do

@@ -1,0 +1,142 @@
+"""GPU parity of the ItemBasedModel's co-listening route (mr_options.ibm_route = 2).
+
+The route counts C[s2][s] = |L_tr(s2) ∩ L_tr(s)| (the distinct-user numerator
+of MusicRecommender.scala:232-235) for every test-visible song s2 at the start
+of each ibm run, then scores rank(u, s) = (1/sqrt c(s)) Σ_{s2 ∈ T(u)} q(s2)·C[s2][s]
+(MR:249-257 in the engine's fixed point). That is the same integer sum as the
+two-hop route's Σ_{v: s ∈ S(v)} Σ_{s2 ∈ T(u) ∩ S(v)} q(s2), so the bar is
+bit-identity with the fixed-point oracle (oracle/fixedpoint.c) and with the
+two-hop route, on every tile width, shard, k and launch.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from musicrecommendation_amd import _lib, synth
+from musicrecommendation_amd.engine import Engine, merge_topk_host
+from musicrecommendation_amd.sharding import song_shards
+from oracle import native
+
+from helpers import synth_fixture
+
+pytestmark = pytest.mark.gpu
+
+
+def run_route(ds, route, *, k=10, dense=True, **kw):
+    with Engine(ds, out_dtype="f64", topk=k, dense=dense, stage1=kw.pop("stage1", "wide"), ibm_route=route,
+                **kw) as e:
+        assert e.ibm_route == ("cooc" if route == "cooc" else "two_hop")
+        e.run("ibm")
+        d = e.dense() if dense else None
+        songs, _, keys = e.topk()
+        return d, songs, keys, (e.song_lo, e.song_hi)
+
+
+def check_route_exact(ds, *, k=10, **kw):
+    d, songs, keys, (lo, hi) = run_route(ds, "cooc", k=k, **kw)
+    exp, ts, tk = native.fp_model(ds, "ibm", song_lo=lo, song_hi=hi, k=k)
+    assert np.array_equal(d, exp, equal_nan=True), "co-listening dense scores differ from the oracle"
+    assert np.array_equal(songs, ts) and np.array_equal(keys, tk), "co-listening top-k differs from the oracle"
+    return d, songs, keys
+
+
+@pytest.mark.parametrize("k", [1, 7, 10, 16])
+@pytest.mark.parametrize("block", [256, 2048, 16384])
+def test_fixtures_and_c2_exact(block, k):
+    for ds in (synth_fixture("tiny")[0], synth_fixture("small")[0], synth.config("c2", n_test=13).dataset()):
+        check_route_exact(ds, k=k, block_songs=block)
+
+
+def test_routes_identical_and_auto():
+    """auto picks the co-listening route on the wide shape; the two routes agree bitwise."""
+    ds = synth.generate_bulk(40_000, 21, 4).dataset()
+    with Engine(ds, out_dtype="f64", topk=10) as e:
+        assert e.shape == "wide" and e.ibm_route == "cooc"
+        assert e.cooc_rows > 0 and e.cooc_pool_entries > 0
+    a = run_route(ds, "cooc")
+    b = run_route(ds, "two_hop")
+    assert np.array_equal(a[0], b[0], equal_nan=True)
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    exp, ts, tk = native.fp_model(ds, "ibm", k=10)
+    assert np.array_equal(a[0], exp, equal_nan=True)
+    assert np.array_equal(a[1], ts) and np.array_equal(a[2], tk)
+    # ubm keeps the two-hop path in the same context
+    with Engine(ds, out_dtype="f64", topk=10) as e:
+        e.run("ubm")
+        got = e.dense()
+    assert np.array_equal(got, native.fp_model(ds, "ubm", k=10)[0], equal_nan=True)
+
+
+@pytest.mark.parametrize("n_shards", [2, 3])
+def test_song_shards(n_shards):
+    """Per-shard index (rows over all test-visible songs, columns = the shard):
+    merged lists identical to one context and to the oracle."""
+    ds = synth.generate_bulk(40_000, 21, 4).dataset()
+    _, ts, tk = native.fp_model(ds, "ibm", k=10)
+    ss, kk = [], []
+    for lo, hi in song_shards(ds, n_shards):
+        d, s, k, _ = run_route(ds, "cooc", song_lo=lo, song_hi=hi)
+        exp = native.fp_model(ds, "ibm", song_lo=lo, song_hi=hi, k=10)[0]
+        assert np.array_equal(d, exp, equal_nan=True)
+        ss.append(s)
+        kk.append(k)
+    ms, _, mk = merge_topk_host(np.stack(ss), np.stack(kk))
+    assert np.array_equal(ms, ts) and np.array_equal(mk, tk)
+
+
+def test_topk_only_graph_and_repeats():
+    """dense = 0, f32, repeated runs and a captured graph of several steps
+    (the per-run index rebuild, its row cursors reset inside the graph)."""
+    ds = synth.generate_bulk(20_000, 64, 7).dataset()
+    _, ts, tk = native.fp_model(ds, "ibm", k=10, dense=False)
+    with Engine(ds, topk=10, dense=False, ibm_route="cooc") as e:
+        for _ in range(3):
+            e.run("ibm")
+            s, _, k = e.topk()
+            assert np.array_equal(s, ts) and np.array_equal(k, tk)
+        e.graph_capture("ibm", 4)
+        e.graph_launch()
+        e.sync()
+        s, _, k = e.topk()
+        assert np.array_equal(s, ts) and np.array_equal(k, tk)
+        # interleaved ubm run, then ibm again
+        e.run("ubm")
+        e.run("ibm")
+        s, _, k = e.topk()
+        assert np.array_equal(s, ts) and np.array_equal(k, tk)
+
+
+def test_cold_and_heavy_users():
+    """Test users whose songs have no train listener (empty rows), a test user
+    with hundreds of songs (several descriptor passes), and one-song users."""
+    rng = np.random.default_rng(11)
+    base = synth.generate_bulk(20_000, 30, 9)
+    heard = np.unique(base.train_s)
+    K = 10 ** 9  # test-user keys past every generated user
+    # user K: 900 distinct train-heard songs; K+1: one song no train user heard; K+2: the most popular song
+    heavy = rng.choice(heard, 900, replace=False)
+    cold = np.array([synth.N_SONG_UNIVERSE + 5])
+    pop = np.array([np.bincount(base.train_s).argmax()])
+    te_u = np.concatenate([np.full(heavy.size, K), [K + 1], [K + 2], base.test_u])
+    te_s = np.concatenate([heavy, cold, pop, base.test_s])
+    t = synth.Triplets(base.train_u, base.train_s, te_u, te_s, base.label_u[:0], base.label_s[:0], base.alpha)
+    ds = t.dataset()
+    check_route_exact(ds, k=10)
+    check_route_exact(ds, k=16, block_songs=4096)
+
+
+def test_route_errors():
+    """ibm_route 2 outside the wide shape is refused with a code; 3 is invalid."""
+    ds, _ = synth_fixture("small")
+    with pytest.raises(_lib.EngineError):
+        Engine(ds, stage1="fused", ibm_route="cooc")
+    with pytest.raises(_lib.EngineError):
+        Engine(ds, stage1="separate", ibm_route="cooc")
+    with Engine(ds, stage1="fused") as e:  # auto on another shape: two-hop
+        assert e.ibm_route == "two_hop"
+    o = _lib.MrOptions()
+    _lib.check(_lib.lib().mr_options_default(ctypes.byref(o)), "defaults")
+    o.ibm_route = 3
+    h = ctypes.c_void_p()
+    assert _lib.lib().mr_create(ctypes.byref(o), ctypes.byref(h)) == _lib.MR_E_INVALID
