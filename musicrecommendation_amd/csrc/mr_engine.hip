@@ -1894,9 +1894,28 @@ struct CoocParams {
   unsigned* pool;
   long long* seg_off;            // [tile][row]
   int* seg_len;                  // [tile][row]
+  const int* rows;               // the rows of this launch (index rows, heaviest first)
+  // k_cooc_light: the shard's train rows (renumbered users, shard-local song ids)
+  const long long* sr_off;
+  const unsigned* sr_songs;
+  const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
 };
 
 __host__ __device__ inline int cooc_build_lds(int bs) { return align16(bs * 4) + 16 * 4 + 16; }
+
+// Light rows (k_cooc_light): an LDS hash table of packed slots
+// ((shard-local song + 1) << kLightCntBits) | count, at most kLightSlots;
+// a row is light when its entry bound fits half the slots, its listener count
+// fits kLightCntBits and the shard's songs fit the key bits.
+constexpr int kLightCntBits = 12;
+constexpr unsigned kLightCntMask = (1u << kLightCntBits) - 1u;
+constexpr int kLightSlots = 32768;
+constexpr int kLightMaxTiles = 256;
+constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
+constexpr int kLightNT = 1024;
+__host__ __device__ inline int cooc_light_lds() {
+  return kLightSlots * 4 + 2 * kLightMaxTiles * 4 + kLightNT * 12 + 16 * 4 + 16;
+}
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
@@ -1906,7 +1925,8 @@ __global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
   int* s_scan = reinterpret_cast<int*>(smem_raw + align16(bs * 4));
   long long* s_base = reinterpret_cast<long long*>(s_scan + 16);
-  const int r = blockIdx.x / p.n_tiles, tile = blockIdx.x - r * p.n_tiles;
+  const int ri = blockIdx.x / p.n_tiles, tile = blockIdx.x - ri * p.n_tiles;
+  const int r = p.rows[ri];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int blo = p.song_lo + tile * bs;
   const int bw = min(p.song_hi, blo + bs) - blo;
@@ -1960,6 +1980,113 @@ __global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
     const unsigned long long m = __ballot(c != 0u);
     if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
     base += __popcll(m);
+  }
+}
+
+// Light index rows: one workgroup per row (instead of one per (row, tile)).
+// The row's listeners' whole shard rows (sr_off / sr_songs) are walked as one
+// flattened list into an LDS hash table of counts (open addressing, linear
+// probing, CAS insert), then the table is emitted tile by tile: per-tile
+// counts, their prefix -> the row's segment of every tile (seg_off / seg_len,
+// empty tiles included), entries placed by LDS cursors (order inside a
+// segment is arbitrary; the consumer's sums are order-free).
+__global__ __launch_bounds__(kLightNT) void k_cooc_light(CoocParams p) {
+  constexpr int NT = kLightNT;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  unsigned* tab = reinterpret_cast<unsigned*>(smem_raw);
+  int* tcnt = reinterpret_cast<int*>(tab + kLightSlots);
+  int* tpos = tcnt + kLightMaxTiles;
+  long long* m_a = reinterpret_cast<long long*>(tpos + kLightMaxTiles);
+  int* m_pre = reinterpret_cast<int*>(m_a + NT);
+  int* s_scan = m_pre + NT + 16;
+  const int r = p.rows[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int S = p.row_slots[r];
+  const unsigned mask = (unsigned)S - 1u;
+  const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
+  for (int i = tid; i < S; i += NT) tab[i] = 0u;
+  for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
+  const int s2 = p.row_song[r];
+  const long long la = p.trs_off[s2];
+  const int n = (int)(p.trs_off[s2 + 1] - la);
+  const int* lst = p.trs_users + la;
+  for (int c0 = 0; c0 < n; c0 += NT) {
+    long long a = 0;
+    int len = 0;
+    if (c0 + tid < n) {
+      const int v = lst[c0 + tid];
+      a = p.sr_off[v];
+      len = (int)(p.sr_off[v + 1] - a);
+    }
+    int total;
+    const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);  // (its barriers also order the zeroing)
+    m_a[tid] = a - pre;
+    m_pre[tid] = pre;
+    if (tid == 0) m_pre[min(NT, n - c0)] = total;
+    __syncthreads();
+    constexpr int U = 4;
+    int cur = -1, ce = 0;
+    long long co = 0;
+    for (int e0 = tid; e0 < total; e0 += U * NT) {
+      unsigned key[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int e = e0 + j * NT;
+        key[j] = ~0u;
+        if (e < total) {
+          while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_a[cur]; }
+          key[j] = p.sr_songs[co + e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (key[j] == ~0u) continue;
+        const unsigned tag = (key[j] + 1u) << kLightCntBits;
+        unsigned h = (key[j] * 2654435761u) >> sh;
+        for (;;) {
+          unsigned x = tab[h];
+          if (x == 0u) {
+            x = atomicCAS(&tab[h], 0u, tag | 1u);
+            if (x == 0u) break;
+          }
+          if ((x & ~kLightCntMask) == tag) { atomicAdd(&tab[h], 1u); break; }
+          h = (h + 1u) & mask;
+        }
+      }
+    }
+    __syncthreads();  // the next chunk rewrites the listener descriptors
+  }
+  // emit: per-tile counts, segment offsets, then the entries
+  const int bs = p.block_songs;
+  for (int i = tid; i < S; i += NT) {
+    const unsigned x = tab[i];
+    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
+  }
+  __syncthreads();
+  if (tid < 64) {  // prefix over <= kLightMaxTiles tiles by one wave
+    int run = 0;
+    for (int t0 = 0; t0 < p.n_tiles; t0 += 64) {
+      const int t = t0 + tid;
+      const int c = t < p.n_tiles ? tcnt[t] : 0;
+      const int inc = wave_incl_scan(c);
+      if (t < p.n_tiles) {
+        tpos[t] = run + inc - c;
+        p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
+        p.seg_len[(size_t)t * p.n_rows + r] = c;
+      }
+      run += __shfl(inc, 63, 64);
+    }
+  }
+  __syncthreads();
+  unsigned* out = p.pool + p.row_base[r];
+  for (int i = tid; i < S; i += NT) {
+    const unsigned x = tab[i];
+    if (x) {
+      const int key = (int)((x >> kLightCntBits) - 1u);
+      const int t = key / bs;
+      const int pos = atomicAdd(&tpos[t], 1);
+      out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
+    }
   }
 }
 
@@ -2204,6 +2331,10 @@ struct mr_ctx {
   DevBuf<int> row_song, te_row, seg_len;
   DevBuf<long long> row_base, seg_off;
   DevBuf<unsigned> row_cur, pool;
+  int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
+  DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
+  DevBuf<long long> sr_off;        // light rows: the shard's train rows
+  DevBuf<unsigned> sr_songs;
 
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
@@ -2217,7 +2348,8 @@ struct mr_ctx {
     flag.release();
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     row_cur.release(); pool.release();
-    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr;
+    rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release();
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -2301,6 +2433,13 @@ int merge_rows_opt() {
 
 // Wide-shape block mapping (ScoreParams.xcd_remap): 1 = tiles of a user on
 // one XCD, 2 = one tile's users per XCD; MR_WIDE_MAP=1/2 overrides.
+// Light index rows by k_cooc_light (default) or every row per (row, tile)
+// (MR_COOC_LIGHT=0: A/B experiments and tests; read at each mr_load).
+bool cooc_light_opt() {
+  const char* e = std::getenv("MR_COOC_LIGHT");
+  return !(e && std::atoi(e) == 0);
+}
+
 int wide_map_opt() {
   static const int m = [] {
     const char* e = std::getenv("MR_WIDE_MAP");
@@ -2729,6 +2868,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   int route = 1;
   std::vector<int32_t> row_song, te_row;
   std::vector<int64_t> row_base;
+  std::vector<int32_t> heavy_rows, light_rows, row_slots;
   int64_t pool_cap = 0;
   {
     const char* why = nullptr;
@@ -2774,6 +2914,19 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           row_base[r] = std::min<int64_t>(sum, width);
         }
       }, 256);
+      // light rows (k_cooc_light): the bound fits half the hash slots
+      const bool light_ok = width <= kLightMaxWidth && n_tiles <= kLightMaxTiles && cooc_light_opt();
+      row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
+      for (int64_t r = 0; r < nr; ++r) {
+        if (light_ok && row_base[r] <= kLightSlots / 2 && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
+          int sl = 1024;
+          while (sl < 2 * row_base[r]) sl <<= 1;
+          row_slots[r] = sl;
+          light_rows.push_back((int32_t)r);
+        } else {
+          heavy_rows.push_back((int32_t)r);
+        }
+      }
       pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
       row_base[nr] = pool_cap;
       size_t free_b = 0, total_b = 0;
@@ -2843,6 +2996,32 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
+    std::vector<int32_t> order(heavy_rows);
+    order.insert(order.end(), light_rows.begin(), light_rows.end());
+    if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
+    if ((rc = dev_upload(c->row_slots, row_slots.data(), row_slots.size(), st))) return rc;
+    if (!light_rows.empty()) {
+      // the shard's train rows, shard-local song ids (k_cooc_light's input)
+      std::vector<int64_t> so((size_t)n_tr + 1, 0);
+      mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
+        for (int64_t v = a; v < b; ++v) {
+          const int32_t* r0 = tr_songs + tr_off[v];
+          const int32_t* r1 = tr_songs + tr_off[v + 1];
+          so[v] = std::lower_bound(r0, r1, hi) - std::lower_bound(r0, r1, lo);
+        }
+      });
+      so[n_tr] = mr_par::exclusive_scan(so.data(), (int64_t)n_tr);
+      mr_par::buffer<uint32_t> ss((size_t)std::max<int64_t>(1, so[n_tr]));
+      mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
+        for (int64_t v = a; v < b; ++v) {
+          const int32_t* r0 = std::lower_bound(tr_songs + tr_off[v], tr_songs + tr_off[v + 1], lo);
+          for (int64_t i = 0; i < so[v + 1] - so[v]; ++i) ss[so[v] + i] = (uint32_t)(r0[i] - lo);
+        }
+      });
+      if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
+      if ((rc = dev_upload(c->sr_songs, ss.data(), (size_t)std::max<int64_t>(1, so[n_tr]), st))) return rc;
+      MR_HIP(hipStreamSynchronize(st));  // so / ss die here
+    }
   }
   if (k > 0) {
     // wide: per-tile candidates of one launch (a neighbour batch; the
@@ -2892,6 +3071,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 4) / 20);
     if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
     c->cooc_lds = (size_t)cooc_build_lds(bs);
+    c->n_heavy = (int)heavy_rows.size();
+    c->n_light = (int)light_rows.size();
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               cooc_light_lds()));
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3008,9 +3191,17 @@ int run_cooc(mr_ctx* c) {
     MR_HIP(hipMemsetAsync(c->row_cur.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
-                  c->seg_off.p, c->seg_len.p};
-    hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_rows * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
-    MR_HIP(hipGetLastError());
+                  c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p};
+    if (c->n_heavy > 0) {
+      hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_heavy * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
+      MR_HIP(hipGetLastError());
+    }
+    if (c->n_light > 0) {
+      CoocParams lp = cp;
+      lp.rows = c->rows_order.p + c->n_heavy;
+      hipLaunchKernelGGL(k_cooc_light, dim3(c->n_light), dim3(kLightNT), (size_t)cooc_light_lds(), st, lp);
+      MR_HIP(hipGetLastError());
+    }
   }
   if (timed) MR_HIP(hipEventRecord(ev[1], st));
   for (int y0 = 0; y0 < c->n_te; y0 += 65528) {

@@ -41,14 +41,25 @@ def check_route_exact(ds, *, k=10, **kw):
     return d, songs, keys
 
 
+@pytest.fixture(params=["light", "tiled"])
+def build_path(request, monkeypatch):
+    """Index rows built by k_cooc_light where they fit (default) or every row
+    per (row, tile) by k_cooc_build (MR_COOC_LIGHT=0, read at mr_load)."""
+    if request.param == "tiled":
+        monkeypatch.setenv("MR_COOC_LIGHT", "0")
+    else:
+        monkeypatch.delenv("MR_COOC_LIGHT", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("k", [1, 7, 10, 16])
 @pytest.mark.parametrize("block", [256, 2048, 16384])
-def test_fixtures_and_c2_exact(block, k):
+def test_fixtures_and_c2_exact(block, k, build_path):
     for ds in (synth_fixture("tiny")[0], synth_fixture("small")[0], synth.config("c2", n_test=13).dataset()):
         check_route_exact(ds, k=k, block_songs=block)
 
 
-def test_routes_identical_and_auto():
+def test_routes_identical_and_auto(build_path):
     """auto picks the co-listening route on the wide shape; the two routes agree bitwise."""
     ds = synth.generate_bulk(40_000, 21, 4).dataset()
     with Engine(ds, out_dtype="f64", topk=10) as e:
@@ -69,7 +80,7 @@ def test_routes_identical_and_auto():
 
 
 @pytest.mark.parametrize("n_shards", [2, 3])
-def test_song_shards(n_shards):
+def test_song_shards(n_shards, build_path):
     """Per-shard index (rows over all test-visible songs, columns = the shard):
     merged lists identical to one context and to the oracle."""
     ds = synth.generate_bulk(40_000, 21, 4).dataset()
@@ -107,7 +118,7 @@ def test_topk_only_graph_and_repeats():
         assert np.array_equal(s, ts) and np.array_equal(k, tk)
 
 
-def test_cold_and_heavy_users():
+def test_cold_and_heavy_users(build_path):
     """Test users whose songs have no train listener (empty rows), a test user
     with hundreds of songs (several descriptor passes), and one-song users."""
     rng = np.random.default_rng(11)
