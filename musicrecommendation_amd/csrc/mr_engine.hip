@@ -1537,7 +1537,7 @@ constexpr int kWideThreads = 1024;
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
 #ifndef MR_COOC_U
-#define MR_COOC_U 8         // co-listening route: pool entries per thread in flight
+#define MR_COOC_U 4         // co-listening route: 16-B pool loads (4 entries) per thread in flight
 #endif
 #ifndef MR_COOC_R
 #define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
@@ -1545,6 +1545,8 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_NT
 #define MR_COOC_NT 1024     // co-listening index build: threads per workgroup
 #endif
+// 16-B vector of 4-B-aligned words (global_load_dwordx4 needs dword alignment only)
+typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Co-listening index entries: (tile-local song << kCoocCntBits) | count, so
 // tiles <= 32768 songs and counts < 131072 (mr_load checks both).
 constexpr int kCoocCntBits = 17;
@@ -1730,28 +1732,47 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       if (tid < ns) { m_off[tid] = off - pre; m_q[tid] = q; m_pre[tid] = pre; }
       if (tid == 0) m_pre[ns] = total;
       __syncthreads();
+      // 4 consecutive entries per thread and load (one 16-B load when they
+      // lie in one segment, else entry by entry), U loads in flight
       constexpr int U = MR_COOC_U;
-      // the thread's current row: entries [cb, ce) at pool[co + e], weight cq
+      // the thread's current row: entries up to ce at pool[co + e], weight cq
       int cur = -1, ce = 0;
       long long co = 0;
       unsigned long long cq = 0ull;
-      for (int e0 = tid; e0 < total; e0 += U * NT) {
-        unsigned x[U];
-        unsigned long long wq[U];
+      for (int e0 = 4 * tid; e0 < total; e0 += 4 * U * NT) {
+        unsigned x[U][4];
+        unsigned long long wq[U][4];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-          const int e = e0 + j * NT;
-          x[j] = 0u;
-          wq[j] = 0ull;
+          const int e = e0 + j * 4 * NT;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { x[j][i] = 0u; wq[j][i] = 0ull; }
           if (e < total) {
             while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_off[cur]; cq = m_q[cur]; }
-            x[j] = p.pool[co + e];
-            wq[j] = cq;
+            if (e + 3 < ce) {
+              const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(p.pool + co + e);
+              x[j][0] = v.x; x[j][1] = v.y; x[j][2] = v.z; x[j][3] = v.w;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) wq[j][i] = cq;
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int ei = e + i;
+                if (ei < total) {
+                  while (ei >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_off[cur]; cq = m_q[cur]; }
+                  x[j][i] = p.pool[co + ei];
+                  wq[j][i] = cq;
+                }
+              }
+            }
           }
         }
 #pragma unroll
         for (int j = 0; j < U; ++j)
-          if (wq[j]) atomicAdd(&acc[x[j] >> kCoocCntBits], (unsigned long long)(x[j] & kCoocCntMask) * wq[j]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (wq[j][i])
+              atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
       }
       __syncthreads();  // the next pass rewrites the descriptors
     }
