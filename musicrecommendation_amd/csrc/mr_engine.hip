@@ -1550,6 +1550,10 @@ typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Co-listening index entries: (tile-local song << kCoocCntBits) | count, so
 // tiles <= 32768 songs and counts < 131072 (mr_load checks both).
 constexpr int kCoocCntBits = 17;
+// seg_len of a dense segment (counts of every song of the tile, u16 / u32)
+constexpr int kCoocDense16 = -1;
+constexpr int kCoocDense32 = -2;
+constexpr int kCoocDenseDiv = 3;  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
 constexpr int kCoocMaxTile = 1 << (32 - kCoocCntBits);
 
@@ -1705,33 +1709,74 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 
   if constexpr (COOC) {
     // stage 2 from the co-listening index: acc[s] += q(s2) * C[s2][s] over
-    // the tile segments of u's index rows, walked as one flattened list
-    // (coalesced pool reads). Descriptors of up to nseg rows per pass live in
-    // the top-k scratch, which is free until the epilogue.
+    // u's index rows' segments in this tile. Dense segments (every song's
+    // count) are summed per song by the thread that owns it, in registers;
+    // sparse segments are walked as one flattened list (coalesced pool reads,
+    // LDS atomics). Descriptors of up to nseg rows per pass live in the top-k
+    // scratch, which is free until the epilogue.
     long long* m_off = reinterpret_cast<long long*>(smem_raw + L.wk);
     unsigned long long* m_q = reinterpret_cast<unsigned long long*>(m_off + p.nseg);
-    int* m_pre = reinterpret_cast<int*>(m_q + p.nseg);
+    long long* d_off = reinterpret_cast<long long*>(m_q + p.nseg);
+    unsigned long long* d_q = reinterpret_cast<unsigned long long*>(d_off + p.nseg);
+    int* m_pre = reinterpret_cast<int*>(d_q + p.nseg);
+    int* d_fmt = m_pre + p.nseg + 1;
     const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
     const int* slen = p.seg_len + (size_t)tile * p.n_rows;
     const long long* soff = p.seg_off + (size_t)tile * p.n_rows;
     for (long long c0 = t0; c0 < t1; c0 += p.nseg) {
       const int ns = (int)min<long long>(p.nseg, t1 - c0);
-      int len = 0;
+      int len = 0, isd = 0, fmt = 0;
       long long off = 0;
       unsigned long long q = 0ull;
       if (tid < ns) {
         const int r = p.te_row[c0 + tid];
         if (r >= 0) {
-          len = slen[r];
+          const int sl = slen[r];
           off = soff[r];
           q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
+          if (sl < 0) { isd = 1; fmt = sl; } else { len = sl; }
         }
       }
-      int total;
+      int total, nd;
       const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
-      if (tid < ns) { m_off[tid] = off - pre; m_q[tid] = q; m_pre[tid] = pre; }
+      const int dpre = block_excl_scan_nt<NT>(isd, &nd, s_scan);
+      if (tid < ns) {
+        m_off[tid] = off - pre;
+        m_q[tid] = q;
+        m_pre[tid] = pre;
+        if (isd) { d_off[dpre] = off; d_q[dpre] = q; d_fmt[dpre] = fmt; }
+      }
       if (tid == 0) m_pre[ns] = total;
       __syncthreads();
+      if (nd > 0) {
+        // 8 songs per thread per block of 8 * NT, every dense row summed in registers
+        for (int b0 = 8 * tid; b0 < bw; b0 += 8 * NT) {
+          unsigned long long a8[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a8[i] = 0ull;
+          for (int d = 0; d < nd; ++d) {
+            const unsigned* seg = p.pool + d_off[d];
+            const unsigned long long qd = d_q[d];
+            unsigned c8[8];
+            if (d_fmt[d] == kCoocDense16) {
+              const uint4 v = *reinterpret_cast<const uint4*>(seg + (b0 >> 1));
+              c8[0] = v.x & 0xffffu; c8[1] = v.x >> 16; c8[2] = v.y & 0xffffu; c8[3] = v.y >> 16;
+              c8[4] = v.z & 0xffffu; c8[5] = v.z >> 16; c8[6] = v.w & 0xffffu; c8[7] = v.w >> 16;
+            } else {
+              const uint4 v0 = *reinterpret_cast<const uint4*>(seg + b0);
+              const uint4 v1 = *reinterpret_cast<const uint4*>(seg + b0 + 4);
+              c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
+              c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (b0 + i < bw) acc[b0 + i] += a8[i];
+        }
+        __syncthreads();  // the sparse walk's atomics may hit any song
+      }
       // 4 consecutive entries per thread and load (one 16-B load when they
       // lie in one segment, else entry by entry), U loads in flight
       constexpr int U = MR_COOC_U;
@@ -1920,6 +1965,8 @@ struct CoocParams {
   const long long* sr_off;
   const unsigned* sr_songs;
   const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
+  int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
+  int force32;                   // 1: dense counts as u32 even below 65536 listeners (tests)
 };
 
 __host__ __device__ inline int cooc_build_lds(int bs) { return align16(bs * 4) + 16 * 4 + 16; }
@@ -1939,7 +1986,7 @@ __host__ __device__ inline int cooc_light_lds() {
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
+__global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {  // 2 workgroups per CU
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
@@ -1985,15 +2032,32 @@ __global__ __launch_bounds__(NT) void k_cooc_build(CoocParams p) {
     base += x < w ? s_scan[x] : 0;
     total += s_scan[x];
   }
+  // Dense segment when at least a third of the tile's songs are non-zero:
+  // every song's count as u16 (listener count < 65536: no count can exceed
+  // it) or u32, no index and no atomics on the consumer side. Reservations
+  // are whole 16-B words (dense segments are read by 16-B loads).
+  const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
+  const bool c16 = n < 65536 && !p.force32;
+  // (u32 dense: whole 32-B words, read 8 songs at a time)
+  const int words = dense ? (c16 ? ((bw + 1) / 2 + 3) & ~3 : (bw + 7) & ~7) : (total + 3) & ~3;
   if (tid == 0) {
-    const unsigned at = total ? atomicAdd(&p.row_cur[r], (unsigned)total) : 0u;
+    const unsigned at = words ? atomicAdd(&p.row_cur[r], (unsigned)words) : 0u;
     const long long off = p.row_base[r] + at;
     p.seg_off[(size_t)tile * p.n_rows + r] = off;
-    p.seg_len[(size_t)tile * p.n_rows + r] = total;
+    p.seg_len[(size_t)tile * p.n_rows + r] = dense ? (c16 ? kCoocDense16 : kCoocDense32) : total;
     s_base[0] = off;
   }
   __syncthreads();
   unsigned* out = p.pool + s_base[0];
+  if (dense) {
+    if (c16) {
+      for (int i = tid; 2 * i < bw; i += NT)
+        out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
+    } else {
+      for (int i = tid; i < bw; i += NT) out[i] = cnt[i];
+    }
+    return;
+  }
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int i0 = wb; i0 < we; i0 += 64) {
     const int i = i0 + lane;
@@ -2353,6 +2417,7 @@ struct mr_ctx {
   DevBuf<long long> row_base, seg_off;
   DevBuf<unsigned> row_cur, pool;
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
+  int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
   DevBuf<long long> sr_off;        // light rows: the shard's train rows
   DevBuf<unsigned> sr_songs;
@@ -2459,6 +2524,17 @@ int merge_rows_opt() {
 bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
   return !(e && std::atoi(e) == 0);
+}
+// Dense-segment rule of k_cooc_build (MR_COOC_DENSE_DIV, default kCoocDenseDiv;
+// 0 = sparse only) and u32 dense counts for every row (MR_COOC_DENSE32=1):
+// experiments and tests, read at each mr_load.
+int cooc_dense_div_opt() {
+  const char* e = std::getenv("MR_COOC_DENSE_DIV");
+  return e ? std::max(0, std::atoi(e)) : kCoocDenseDiv;
+}
+int cooc_dense32_opt() {
+  const char* e = std::getenv("MR_COOC_DENSE32");
+  return e && std::atoi(e) == 1 ? 1 : 0;
 }
 
 int wide_map_opt() {
@@ -2890,6 +2966,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   std::vector<int32_t> row_song, te_row;
   std::vector<int64_t> row_base;
   std::vector<int32_t> heavy_rows, light_rows, row_slots;
+  int dense_div = kCoocDenseDiv;
   int64_t pool_cap = 0;
   {
     const char* why = nullptr;
@@ -2932,11 +3009,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           const int s2 = row_song[r];
           int64_t sum = 0;
           for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1] && sum < width; ++i) sum += deg[trs_users[i]];
-          row_base[r] = std::min<int64_t>(sum, width);
+          row_base[r] = std::min<int64_t>(sum, width);  // the row's non-zeros: its sparse bound
         }
       }, 256);
       // light rows (k_cooc_light): the bound fits half the hash slots
       const bool light_ok = width <= kLightMaxWidth && n_tiles <= kLightMaxTiles && cooc_light_opt();
+      dense_div = cooc_dense_div_opt();
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
         if (light_ok && row_base[r] <= kLightSlots / 2 && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
@@ -2944,7 +3022,14 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           while (sl < 2 * row_base[r]) sl <<= 1;
           row_slots[r] = sl;
           light_rows.push_back((int32_t)r);
+          row_base[r] = (row_base[r] + 3) & ~(int64_t)3;
         } else {
+          // k_cooc_build: a tile's segment is sparse (its non-zeros) or dense
+          // (<= kCoocDenseDiv x its non-zeros, <= the tile's songs), in whole
+          // 16-B words (32-B for u32 counts)
+          const int64_t nz = row_base[r];
+          const int64_t dn = std::max<int64_t>(1, std::min<int64_t>(dense_div, width)) * nz;
+          row_base[r] = ((std::min<int64_t>(width, dn) + 3) & ~(int64_t)3) + 8 * (int64_t)n_tiles;
           heavy_rows.push_back((int32_t)r);
         }
       }
@@ -3087,12 +3172,14 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if (route == 2) {
     c->n_rows = (int)row_song.size();
     c->pool_cap = pool_cap;
-    // the score kernel's row descriptors (20 B each) in its top-k scratch
+    // the score kernel's row descriptors (40 B each: sparse + dense views) in its top-k scratch
     const WideLds<kWideThreads> WL = wide_lds<kWideThreads>(bs, k, n_chunks);
-    c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 4) / 20);
+    c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 8) / 40);
     if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
     c->cooc_lds = (size_t)cooc_build_lds(bs);
     c->n_heavy = (int)heavy_rows.size();
+    c->dense_div = dense_div;
+    c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light, hipFuncAttributeMaxDynamicSharedMemorySize,
                                cooc_light_lds()));
@@ -3107,8 +3194,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->merge_lds));
   }
 #ifdef MR_STAMPS
-  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * (batch + 8) * kStampSlots))) return rc;
-  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * (batch + 8) * kStampSlots * 8, st));
+  const size_t stamp_users = (size_t)std::max(batch, route == 2 ? std::min(n_te, 65528) : 0) + 8;
+  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * stamp_users * kStampSlots))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * stamp_users * kStampSlots * 8, st));
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
   trace("upload");
@@ -3212,7 +3300,8 @@ int run_cooc(mr_ctx* c) {
     MR_HIP(hipMemsetAsync(c->row_cur.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
-                  c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p};
+                  c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
+                  c->dense_div, c->force32};
     if (c->n_heavy > 0) {
       hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_heavy * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
       MR_HIP(hipGetLastError());
@@ -3244,7 +3333,7 @@ int run_cooc(mr_ctx* c) {
     sp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p;
     sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
     sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
-    sp.stamps = nullptr;  // the stamps buffer is sized for one neighbour batch
+    sp.stamps = y0 == 0 ? c->stamps.p : nullptr;  // diagnostic build: the first launch
     sp.topk_lists = c->opt.topk_lists;
     hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(kWideThreads), c->score_lds, st, sp);
     MR_HIP(hipGetLastError());

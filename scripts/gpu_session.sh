@@ -85,6 +85,16 @@ case ",$STEPS," in *,c4route,*)
     run bench_c4_$r 900 python -u bench.py --config c4 --steps 5 --warmup 2 --no-e2e --no-cpu-baseline --no-north-star --ibm-route $r
   done ;;
 esac
+# C4 ibm over library variants (scripts/build_variant.py): VARIANTS="prod u2 u8"
+case ",$STEPS," in *,c4var,*)
+  for v in ${VARIANTS:-prod}; do
+    lib=$v; [ "$v" = prod ] && lib=""
+    export TMPDIR=/tmp
+    MR_ENGINE_LIB=$lib run c4var_$v 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4var_$v" -o p -- python3 "$ROOT/bench.py" --config c4 --steps 5 --warmup 2 --no-e2e --no-cpu-baseline --no-north-star
+  done ;;
+esac
+# phase stamps of the wide / co-listening scoring kernel: LSTAMPS="1009318 2000 ibm"
+case ",$STEPS," in *,lstamps,*) run lstamps 600 python -u scripts/large_stamps.py ${LSTAMPS:-1009318 2000 ibm} ;; esac
 case ",$STEPS," in *,profc4cooc,*)
   export TMPDIR=/tmp
   run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;

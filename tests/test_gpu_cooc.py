@@ -41,14 +41,25 @@ def check_route_exact(ds, *, k=10, **kw):
     return d, songs, keys
 
 
-@pytest.fixture(params=["light", "tiled"])
+# Index build paths (engine environment read at mr_load): light rows by the
+# LDS hash (default) or every row per (row, tile) (MR_COOC_LIGHT=0); tile
+# segments dense when a third of the songs are non-zero (default), always
+# (MR_COOC_DENSE_DIV=1000000, u16 or, with MR_COOC_DENSE32=1, u32 counts) or never (0).
+BUILD_PATHS = {
+    "light": {},
+    "tiled": {"MR_COOC_LIGHT": "0"},
+    "sparse": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "0"},
+    "dense16": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000"},
+    "dense32": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000", "MR_COOC_DENSE32": "1"},
+}
+
+
+@pytest.fixture(params=list(BUILD_PATHS))
 def build_path(request, monkeypatch):
-    """Index rows built by k_cooc_light where they fit (default) or every row
-    per (row, tile) by k_cooc_build (MR_COOC_LIGHT=0, read at mr_load)."""
-    if request.param == "tiled":
-        monkeypatch.setenv("MR_COOC_LIGHT", "0")
-    else:
-        monkeypatch.delenv("MR_COOC_LIGHT", raising=False)
+    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32"):
+        monkeypatch.delenv(key, raising=False)
+    for key, val in BUILD_PATHS[request.param].items():
+        monkeypatch.setenv(key, val)
     return request.param
 
 
