@@ -172,6 +172,12 @@ __device__ __forceinline__ void stamp_at(long long* sb, int i) {
   }
 #endif
 }
+// k_cooc_build's stamps: s_memrealtime only, 8 slots per workgroup
+__device__ __forceinline__ void stamp_rt(long long* sb, int i) {
+#ifdef MR_STAMPS
+  if (sb && threadIdx.x == 0) sb[i] = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
+}
 #ifdef MR_STAMPS
 #define MR_STAMP(i) stamp_at(p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr, (i))
 #else
@@ -1539,6 +1545,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_U
 #define MR_COOC_U 4         // co-listening route: 16-B pool loads (4 entries) per thread in flight
 #endif
+#ifndef MR_COOC_DU
+#define MR_COOC_DU 4        // co-listening route: dense rows whose 16-B loads are issued together
+#endif
 #ifndef MR_COOC_R
 #define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
 #endif
@@ -1672,6 +1681,9 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     const int pidx = (lin & 7) * per_xcd + slot;
     tile = pidx / gridDim.y;
     bu = pidx - tile * gridDim.y;
+  } else if (p.xcd_remap == 3) {  // tile-major: every XCD on the same tile at once
+    tile = lin / gridDim.y;
+    bu = lin - tile * gridDim.y;
   } else {
     bu = (slot / p.n_tiles) * 8 + (lin & 7);
     tile = slot % p.n_tiles;
@@ -1754,22 +1766,43 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           unsigned long long a8[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) a8[i] = 0ull;
-          for (int d = 0; d < nd; ++d) {
-            const unsigned* seg = p.pool + d_off[d];
-            const unsigned long long qd = d_q[d];
-            unsigned c8[8];
-            if (d_fmt[d] == kCoocDense16) {
-              const uint4 v = *reinterpret_cast<const uint4*>(seg + (b0 >> 1));
-              c8[0] = v.x & 0xffffu; c8[1] = v.x >> 16; c8[2] = v.y & 0xffffu; c8[3] = v.y >> 16;
-              c8[4] = v.z & 0xffffu; c8[5] = v.z >> 16; c8[6] = v.w & 0xffffu; c8[7] = v.w >> 16;
-            } else {
-              const uint4 v0 = *reinterpret_cast<const uint4*>(seg + b0);
-              const uint4 v1 = *reinterpret_cast<const uint4*>(seg + b0 + 4);
-              c8[0] = v0.x; c8[1] = v0.y; c8[2] = v0.z; c8[3] = v0.w;
-              c8[4] = v1.x; c8[5] = v1.y; c8[6] = v1.z; c8[7] = v1.w;
+          // DU dense rows per step, their loads issued together
+          constexpr int DU = MR_COOC_DU;
+          for (int d0 = 0; d0 < nd; d0 += DU) {
+            uint4 v0[DU], v1[DU];
+            unsigned long long qd[DU];
+            bool w16[DU];
+#pragma unroll
+            for (int j = 0; j < DU; ++j) {
+              const int d = d0 + j;
+              qd[j] = 0ull;
+              w16[j] = true;
+              v0[j] = v1[j] = make_uint4(0u, 0u, 0u, 0u);
+              if (d < nd) {
+                const unsigned* seg = p.pool + d_off[d];
+                qd[j] = d_q[d];
+                w16[j] = d_fmt[d] == kCoocDense16;
+                if (w16[j]) {
+                  v0[j] = *reinterpret_cast<const uint4*>(seg + (b0 >> 1));
+                } else {
+                  v0[j] = *reinterpret_cast<const uint4*>(seg + b0);
+                  v1[j] = *reinterpret_cast<const uint4*>(seg + b0 + 4);
+                }
+              }
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd;
+            for (int j = 0; j < DU; ++j) {
+              unsigned c8[8];
+              if (w16[j]) {
+                c8[0] = v0[j].x & 0xffffu; c8[1] = v0[j].x >> 16; c8[2] = v0[j].y & 0xffffu; c8[3] = v0[j].y >> 16;
+                c8[4] = v0[j].z & 0xffffu; c8[5] = v0[j].z >> 16; c8[6] = v0[j].w & 0xffffu; c8[7] = v0[j].w >> 16;
+              } else {
+                c8[0] = v0[j].x; c8[1] = v0[j].y; c8[2] = v0[j].z; c8[3] = v0[j].w;
+                c8[4] = v1[j].x; c8[5] = v1[j].y; c8[6] = v1[j].z; c8[7] = v1[j].w;
+              }
+#pragma unroll
+              for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd[j];
+            }
           }
 #pragma unroll
           for (int i = 0; i < 8; ++i)
@@ -1967,6 +2000,7 @@ struct CoocParams {
   const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
   int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
   int force32;                   // 1: dense counts as u32 even below 65536 listeners (tests)
+  long long* stamps;             // diagnostic build: [workgroup][8] s_memrealtime at phase ends
 };
 
 __host__ __device__ inline int cooc_build_lds(int bs) { return align16(bs * 4) + 16 * 4 + 16; }
@@ -1998,8 +2032,11 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int blo = p.song_lo + tile * bs;
   const int bw = min(p.song_hi, blo + bs) - blo;
+  long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  stamp_rt(sb, 0);
   for (int i = tid; i < bw; i += NT) cnt[i] = 0u;
   __syncthreads();
+  stamp_rt(sb, 1);
   const int s2 = p.row_song[r];
   const long long a = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - a);
@@ -2015,6 +2052,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   };
   walk_tile_lists<NT, R, kSeg, unsigned, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs, cnt);
   __syncthreads();
+  stamp_rt(sb, 2);
   // compaction: wave w owns songs [wb, we) (a multiple of 64 wide), counted by
   // ballots, then written in song order at the wave's offset
   const int q4 = (bw + NT - 1) / NT * 64;
@@ -2048,6 +2086,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
     s_base[0] = off;
   }
   __syncthreads();
+  stamp_rt(sb, 3);
+  if (sb && tid == 0) sb[6] = n;
   unsigned* out = p.pool + s_base[0];
   if (dense) {
     if (c16) {
@@ -2056,6 +2096,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
     } else {
       for (int i = tid; i < bw; i += NT) out[i] = cnt[i];
     }
+    stamp_rt(sb, 4);
+    if (sb && tid == 0) sb[5] = 1;  // dense
     return;
   }
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -2066,6 +2108,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
     if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
     base += __popcll(m);
   }
+  stamp_rt(sb, 4);
 }
 
 // Light index rows: one workgroup per row (instead of one per (row, tile)).
@@ -2418,6 +2461,7 @@ struct mr_ctx {
   DevBuf<unsigned> row_cur, pool;
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
+  size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
   DevBuf<long long> sr_off;        // light rows: the shard's train rows
   DevBuf<unsigned> sr_songs;
@@ -2540,7 +2584,8 @@ int cooc_dense32_opt() {
 int wide_map_opt() {
   static const int m = [] {
     const char* e = std::getenv("MR_WIDE_MAP");
-    return e && std::atoi(e) == 1 ? 1 : (e && std::atoi(e) == 2 ? 2 : kWideMapDefault);
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 3 ? v : kWideMapDefault;
   }();
   return m;
 }
@@ -3194,9 +3239,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                (int)c->merge_lds));
   }
 #ifdef MR_STAMPS
+  // scoring workgroups' slots, then (co-listening route) 8 per k_cooc_build workgroup
   const size_t stamp_users = (size_t)std::max(batch, route == 2 ? std::min(n_te, 65528) : 0) + 8;
-  if ((rc = dev_alloc(c->stamps, (size_t)n_tiles * stamp_users * kStampSlots))) return rc;
-  MR_HIP(hipMemsetAsync(c->stamps.p, 0, (size_t)n_tiles * stamp_users * kStampSlots * 8, st));
+  const size_t n_stamps = (size_t)n_tiles * stamp_users * kStampSlots + (size_t)heavy_rows.size() * n_tiles * 8;
+  if ((rc = dev_alloc(c->stamps, n_stamps))) return rc;
+  MR_HIP(hipMemsetAsync(c->stamps.p, 0, n_stamps * 8, st));
+  c->bstamp_off = (size_t)n_tiles * stamp_users * kStampSlots;
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
   trace("upload");
@@ -3301,7 +3349,7 @@ int run_cooc(mr_ctx* c) {
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
-                  c->dense_div, c->force32};
+                  c->dense_div, c->force32, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr};
     if (c->n_heavy > 0) {
       hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_heavy * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
       MR_HIP(hipGetLastError());

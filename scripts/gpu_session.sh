@@ -94,7 +94,15 @@ case ",$STEPS," in *,c4var,*)
   done ;;
 esac
 # phase stamps of the wide / co-listening scoring kernel: LSTAMPS="1009318 2000 ibm"
+case ",$STEPS," in *,cstamps,*) run cstamps 600 python -u scripts/cooc_stamps.py ${CSTAMPS:-} ;; esac
 case ",$STEPS," in *,lstamps,*) run lstamps 600 python -u scripts/large_stamps.py ${LSTAMPS:-1009318 2000 ibm} ;; esac
+# C4 ibm per wide-kernel block map (MR_WIDE_MAP): MAPS="1 2 3"
+case ",$STEPS," in *,c4map,*)
+  export TMPDIR=/tmp
+  for m in ${MAPS:-1 2 3}; do
+    MR_WIDE_MAP=$m run c4map_$m 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4map_$m" -o p -- python3 "$ROOT/bench.py" --config c4 --steps 5 --warmup 2 --no-e2e --no-cpu-baseline --no-north-star
+  done ;;
+esac
 case ",$STEPS," in *,profc4cooc,*)
   export TMPDIR=/tmp
   run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;
