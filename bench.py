@@ -81,6 +81,23 @@ def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
     return {"neighbours": b1, "score": b2, "merge": 12 * k * ds.n_test}
 
 
+def cooc_bytes(eng, ds, out_bytes: int = 4, k: int = 10):
+    """Byte model of the ItemBasedModel's co-listening route,
+    from the engine's counts of the last ibm run (mr_cooc_stats):
+      build    4 Σ_rows (c_tr(s2) + Σ_{v∈L_tr(s2)} |S(v) ∩ shard|)   read each index row's
+               listeners and their songs once (4-B ids)
+               + 4 nnz(index)                                        write the index (4-B entries)
+      score    4 Σ_u Σ_{s2∈T(u)} nnz(row s2)                          read u's rows
+               + per user 4 n_s + out_bytes (n_s − |T(u)|)            scales + dense row
+      merge    12 k per user"""
+    index_nnz, consumed, build_reads = eng.cooc_stats()
+    n_s = eng.width
+    te_n = np.diff(ds.te_off)
+    return {"build": 4 * build_reads + 4 * index_nnz,
+            "score": 4 * consumed + int(4 * n_s * ds.n_test + out_bytes * (n_s * ds.n_test - te_n.sum())),
+            "merge": 12 * k * ds.n_test}
+
+
 def kernel_bytes(ab, fused: bool):
     """Per-launch algorithmic bytes of the launched kernels: the fused shape
     runs all three stages in k_score; the separate shape runs stage 1 in
@@ -633,7 +650,9 @@ def main() -> None:
         ns = north_star(args, world, rank, local)
     if rank == 0:
         value = pairs_all / elapsed_max
-        ab_stage = algorithmic_bytes(ds, 4 if dense_out else 0, 10)
+        cooc = args.model == "ibm" and eng.ibm_route == "cooc"
+        ab_stage = (cooc_bytes(eng, ds, 4 if dense_out else 0, 10) if cooc
+                    else algorithmic_bytes(ds, 4 if dense_out else 0, 10))
         if eng.fused:
             # one kernel per step: the window's mean is that kernel's mean launch
             # duration (plus the launch gaps, which the rocprof summary excludes)
@@ -654,8 +673,12 @@ def main() -> None:
         if traffic is None and os.path.exists(pmc_file) and world == 1 and args.inflight == 1:
             with open(pmc_file) as f:
                 pmc = json.load(f)
-            traffic = pmc.get("traffic_bytes_per_launch")
-            traffic_src = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command)"
+            # counters of the same ibm route only (a wide-shape file without the key is two-hop)
+            route = eng.ibm_route if (args.model == "ibm" and eng.shape == "wide") else None
+            if route is None or (pmc.get("ibm_route") or "two_hop") == route:
+                traffic = pmc.get("traffic_bytes_per_launch")
+                traffic_src = (f"profiles/pmc_{args.config}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                               f"of this command)")
         # quality companions on the last step's outputs (host-side, untimed)
         from musicrecommendation_amd import evaluation
 
@@ -698,9 +721,12 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
-                           "separate": "k_neighbours + k_score (per step)",
-                           "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)"}[eng.shape],
+                "kernel": ("k_cooc_build + k_cooc_light + k_score_wide<cooc> + k_topk_merge (per step)" if cooc else
+                           {"fused": "k_score (fused: stages 1+2+3, one launch per step)",
+                            "separate": "k_neighbours + k_score (per step)",
+                            "wide": "k_neighbours + k_score_wide + k_topk_merge (per step)"}[eng.shape]),
+                "byte_model": ("co-listening route (bench.cooc_bytes: index build + rows read per user)" if cooc
+                               else "two-hop (bench.algorithmic_bytes, SURVEY.md §8d)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -718,7 +744,8 @@ def main() -> None:
                 "timing": f"HIP events on the engine stream around the {args.steps} timed steps "
                           f"({n_launch} scoring launches; avg_launch_us = device time per step)",
             },
-            "launch": {"shape": eng.shape, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles},
+            "launch": {"shape": eng.shape, "block_songs": eng.block_songs, "n_tiles": eng.n_tiles,
+                       "ibm_route": eng.ibm_route},
             "step_algorithmic_bytes": step_bytes,
             "step_GBps": step_bytes / (elapsed_max / args.steps) / 1e9,
             "mAP@10": map10,

@@ -1551,6 +1551,12 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_R
 #define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
 #endif
+#ifndef MR_COOC_NT16
+#define MR_COOC_NT16 512    // co-listening index build, u16-pair counters: threads per workgroup (4 per CU)
+#endif
+#ifndef MR_COOC_P16
+#define MR_COOC_P16 1       // 0: every heavy row with u32 counters (A/B)
+#endif
 #ifndef MR_COOC_NT
 #define MR_COOC_NT 1024     // co-listening index build: threads per workgroup
 #endif
@@ -1574,9 +1580,9 @@ constexpr int kCoocMaxTile = 1 << (32 - kCoocCntBits);
 // iteration. Used by the two-hop scoring (list = the test user's neighbours,
 // w = their int64 weights) and by the co-listening index build (list = one
 // song's train listeners, w = 1).
-template <int NT, int R, int kSeg, typename AccT, typename WT, typename LoadList>
+template <int NT, int R, int kSeg, typename WT, typename LoadList, typename Add>
 __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& load_list, const int* toff_t,
-                                                const unsigned short* tsongs, AccT* acc) {
+                                                const unsigned short* tsongs, Add&& add) {
   // Software pipeline over iterations: iteration i gathers its segments
   // while the toff pairs of i+1 and the list entries of i+2 are in flight
   // (one memory latency covers the three dependent levels).
@@ -1628,13 +1634,13 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
           const int e = (j & 3) + so[r];  // 0..6: word j/4 or the next one
           const uint2 wv = e >= 4 ? sw[r][(j >> 2) + 1] : sw[r][j >> 2];
           const unsigned x = ((e & 3) < 2 ? wv.x : wv.y) >> ((e & 1) * 16);
-          atomicAdd(&acc[x & 0xffffu], q0[r]);
+          add(x & 0xffffu, q0[r]);
         }
       }
 #else
 #pragma unroll
       for (int j = 0; j < kSeg; ++j)
-        if (sg[r][j] >= 0) atomicAdd(&acc[sg[r][j]], q0[r]);
+        if (sg[r][j] >= 0) add((unsigned)sg[r][j], q0[r]);
 #endif
       for (int x0 = a0[r] + kSeg; x0 < b0[r]; x0 += kSeg) {
         int st[kSeg];
@@ -1642,7 +1648,7 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
         for (int j = 0; j < kSeg; ++j) st[j] = x0 + j < b0[r] ? (int)tsongs[x0 + j] : -1;
 #pragma unroll
         for (int j = 0; j < kSeg; ++j)
-          if (st[j] >= 0) atomicAdd(&acc[st[j]], q0[r]);
+          if (st[j] >= 0) add((unsigned)st[j], q0[r]);
       }
     }
 #pragma unroll
@@ -1875,8 +1881,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     };
-    walk_tile_lists<NT, R, kSeg, unsigned long long, unsigned long long>(tid, cnt, load_list,
-                                                                         p.toff + (size_t)tile * p.n_tr, p.tsongs, acc);
+    walk_tile_lists<NT, R, kSeg, unsigned long long>(tid, cnt, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
+                                                     [&](unsigned x, unsigned long long q) { atomicAdd(&acc[x], q); });
   }
   __syncthreads();
   MR_STAMP(2);
@@ -2001,9 +2007,13 @@ struct CoocParams {
   int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
   int force32;                   // 1: dense counts as u32 even below 65536 listeners (tests)
   long long* stamps;             // diagnostic build: [workgroup][8] s_memrealtime at phase ends
+  unsigned* row_nnz;             // [n_rows] non-zero counts of the row over the shard (zeroed per run)
 };
 
-__host__ __device__ inline int cooc_build_lds(int bs) { return align16(bs * 4) + 16 * 4 + 16; }
+template <bool P16>
+__host__ __device__ inline int cooc_words(int bs) { return P16 ? (bs + 1) / 2 : bs; }
+template <bool P16>
+__host__ __device__ inline int cooc_build_lds(int bs) { return align16(cooc_words<P16>(bs) * 4) + 16 * 4 + 16; }
 
 // Light rows (k_cooc_light): an LDS hash table of packed slots
 // ((shard-local song + 1) << kLightCntBits) | count, at most kLightSlots;
@@ -2019,13 +2029,19 @@ __host__ __device__ inline int cooc_light_lds() {
   return kLightSlots * 4 + 2 * kLightMaxTiles * 4 + kLightNT * 12 + 16 * 4 + 16;
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {  // 2 workgroups per CU
+// P16: two u16 counters per LDS word (rows with < 65536 listeners: half the
+// LDS, twice the workgroups per CU), else one u32 counter per song.
+template <int NT, bool P16>
+__global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(CoocParams p) {
   constexpr int NW = NT / 64;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int bs = p.block_songs;
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
-  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(bs * 4));
+  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(cooc_words<P16>(bs) * 4));
+  auto count_of = [&](int i) -> unsigned {
+    if constexpr (P16) return (cnt[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
+    else return cnt[i];
+  };
   long long* s_base = reinterpret_cast<long long*>(s_scan + 16);
   const int ri = blockIdx.x / p.n_tiles, tile = blockIdx.x - ri * p.n_tiles;
   const int r = p.rows[ri];
@@ -2034,7 +2050,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   const int bw = min(p.song_hi, blo + bs) - blo;
   long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
   stamp_rt(sb, 0);
-  for (int i = tid; i < bw; i += NT) cnt[i] = 0u;
+  for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
   __syncthreads();
   stamp_rt(sb, 1);
   const int s2 = p.row_song[r];
@@ -2050,7 +2066,11 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
       q[j] = 1u;
     }
   };
-  walk_tile_lists<NT, R, kSeg, unsigned, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs, cnt);
+  walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
+                                         [&](unsigned x, unsigned) {
+                                           if constexpr (P16) atomicAdd(&cnt[x >> 1], 1u << ((x & 1) << 4));
+                                           else atomicAdd(&cnt[x], 1u);
+                                         });
   __syncthreads();
   stamp_rt(sb, 2);
   // compaction: wave w owns songs [wb, we) (a multiple of 64 wide), counted by
@@ -2060,7 +2080,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   int nz = 0;
   for (int i0 = wb; i0 < we; i0 += 64) {
     const int i = i0 + lane;
-    nz += __popcll(__ballot(i < we && cnt[i] != 0u));
+    nz += __popcll(__ballot(i < we && count_of(i) != 0u));
   }
   if (lane == 0) s_scan[w] = nz;
   __syncthreads();
@@ -2079,6 +2099,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   // (u32 dense: whole 32-B words, read 8 songs at a time)
   const int words = dense ? (c16 ? ((bw + 1) / 2 + 3) & ~3 : (bw + 7) & ~7) : (total + 3) & ~3;
   if (tid == 0) {
+    if (total) atomicAdd(&p.row_nnz[r], (unsigned)total);
     const unsigned at = words ? atomicAdd(&p.row_cur[r], (unsigned)words) : 0u;
     const long long off = p.row_base[r] + at;
     p.seg_off[(size_t)tile * p.n_rows + r] = off;
@@ -2091,10 +2112,12 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   unsigned* out = p.pool + s_base[0];
   if (dense) {
     if (c16) {
-      for (int i = tid; 2 * i < bw; i += NT)
-        out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
+      for (int i = tid; 2 * i < bw; i += NT) {
+        if constexpr (P16) out[i] = cnt[i];  // the LDS words are the u16 pairs already
+        else out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
+      }
     } else {
-      for (int i = tid; i < bw; i += NT) out[i] = cnt[i];
+      for (int i = tid; i < bw; i += NT) out[i] = count_of(i);
     }
     stamp_rt(sb, 4);
     if (sb && tid == 0) sb[5] = 1;  // dense
@@ -2103,7 +2126,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 256) void k_cooc_build(CoocParams p) {
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int i0 = wb; i0 < we; i0 += 64) {
     const int i = i0 + lane;
-    const unsigned c = i < we ? cnt[i] : 0u;
+    const unsigned c = i < we ? count_of(i) : 0u;
     const unsigned long long m = __ballot(c != 0u);
     if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
     base += __popcll(m);
@@ -2193,6 +2216,11 @@ __global__ __launch_bounds__(kLightNT) void k_cooc_light(CoocParams p) {
   __syncthreads();
   if (tid < 64) {  // prefix over <= kLightMaxTiles tiles by one wave
     int run = 0;
+    if (tid == 0) {
+      int nz = 0;
+      for (int t = 0; t < p.n_tiles; ++t) nz += tcnt[t];
+      p.row_nnz[r] = (unsigned)nz;
+    }
     for (int t0 = 0; t0 < p.n_tiles; t0 += 64) {
       const int t = t0 + tid;
       const int c = t < p.n_tiles ? tcnt[t] : 0;
@@ -2459,7 +2487,11 @@ struct mr_ctx {
   DevBuf<int> row_song, te_row, seg_len;
   DevBuf<long long> row_base, seg_off;
   DevBuf<unsigned> row_cur, pool;
+  DevBuf<unsigned> row_nnz;        // per run: each index row's non-zeros over the shard
+  std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
+  long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
+  int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
@@ -2478,8 +2510,9 @@ struct mr_ctx {
     flag.release();
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     row_cur.release(); pool.release();
-    rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release();
-    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = 0;
+    rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
+    row_users.clear(); build_reads = 0;
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -3012,6 +3045,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   std::vector<int64_t> row_base;
   std::vector<int32_t> heavy_rows, light_rows, row_slots;
   int dense_div = kCoocDenseDiv;
+  int n_heavy32 = 0;
+  std::vector<int64_t> row_reads;
   int64_t pool_cap = 0;
   {
     const char* why = nullptr;
@@ -3049,11 +3084,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       });
       const int64_t nr = (int64_t)row_song.size();
       row_base.assign((size_t)nr + 1, 0);
+      row_reads.assign((size_t)nr, 0);
       mr_par::parallel_for(nr, [&](int64_t a, int64_t b, int) {
         for (int64_t r = a; r < b; ++r) {
           const int s2 = row_song[r];
           int64_t sum = 0;
-          for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1] && sum < width; ++i) sum += deg[trs_users[i]];
+          for (int64_t i = trs_off[s2]; i < trs_off[s2 + 1]; ++i) sum += deg[trs_users[i]];
+          row_reads[r] = (trs_off[s2 + 1] - trs_off[s2]) + sum;
           row_base[r] = std::min<int64_t>(sum, width);  // the row's non-zeros: its sparse bound
         }
       }, 256);
@@ -3078,6 +3115,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           heavy_rows.push_back((int32_t)r);
         }
       }
+      // heavy rows whose counts may pass 65535 first (u32 counters), the rest
+      // keep their order (u16-pair counters, k_cooc_build<.., true>)
+      std::stable_partition(heavy_rows.begin(), heavy_rows.end(), [&](int32_t r) {
+        return !MR_COOC_P16 || col_tr[row_song[r]] >= 65536;
+      });
+      for (int32_t r : heavy_rows) n_heavy32 += (!MR_COOC_P16 || col_tr[row_song[r]] >= 65536) ? 1 : 0;
       pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
       row_base[nr] = pool_cap;
       size_t free_b = 0, total_b = 0;
@@ -3144,6 +3187,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_upload(c->te_row, te_row.data(), te_row.size(), st))) return rc;
     if ((rc = dev_upload(c->row_base, reinterpret_cast<const long long*>(row_base.data()), nr + 1, st))) return rc;
     if ((rc = dev_alloc(c->row_cur, nr))) return rc;
+    if ((rc = dev_alloc(c->row_nnz, nr))) return rc;
     if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
@@ -3221,8 +3265,14 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     const WideLds<kWideThreads> WL = wide_lds<kWideThreads>(bs, k, n_chunks);
     c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 8) / 40);
     if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
-    c->cooc_lds = (size_t)cooc_build_lds(bs);
+    c->cooc_lds = (size_t)cooc_build_lds<false>(bs);
     c->n_heavy = (int)heavy_rows.size();
+    c->build_reads = 0;
+    for (int64_t x : row_reads) c->build_reads += x;
+    c->row_users.assign(row_song.size(), 0);
+    for (size_t i = 0; i < (size_t)d->te_off[n_te]; ++i)
+      if (te_row[i] >= 0) c->row_users[te_row[i]]++;
+    c->n_heavy32 = n_heavy32;
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
@@ -3230,8 +3280,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
                                cooc_light_lds()));
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
-    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->cooc_lds));
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               cooc_build_lds<true>(bs)));
   }
   if (wide && k > 0) {
     c->merge_lds = (size_t)merge_lds_bytes(k);
@@ -3265,6 +3317,26 @@ int mr_route_info(const mr_ctx* c, int32_t* route, int32_t* n_rows, int64_t* poo
   if (route) *route = c->ibm_route;
   if (n_rows) *n_rows = c->n_rows;
   if (pool_entries) *pool_entries = c->pool_cap;
+  return MR_OK;
+}
+
+int mr_cooc_stats(mr_ctx* c, int64_t* index_nnz, int64_t* consumed, int64_t* build_reads) {
+  if (!c) return fail(MR_E_INVALID, "null context");
+  if (!c->loaded || c->ibm_route != 2) return fail(MR_E_STATE, "mr_cooc_stats needs a context on ibm_route 2");
+  if (!c->ran || c->last_model != MR_IBM) return fail(MR_E_STATE, "mr_cooc_stats before an ibm run");
+  MR_HIP(hipSetDevice(c->opt.device));
+  std::vector<unsigned> nnz((size_t)std::max(1, c->n_rows), 0u);
+  if (c->n_rows > 0)
+    MR_HIP(hipMemcpyAsync(nnz.data(), c->row_nnz.p, (size_t)c->n_rows * 4, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  int64_t tot = 0, use = 0;
+  for (int r = 0; r < c->n_rows; ++r) {
+    tot += nnz[r];
+    use += (int64_t)nnz[r] * c->row_users[r];
+  }
+  if (index_nnz) *index_nnz = tot;
+  if (consumed) *consumed = use;
+  if (build_reads) *build_reads = c->build_reads;
   return MR_OK;
 }
 
@@ -3346,12 +3418,24 @@ int run_cooc(mr_ctx* c) {
   }
   if (c->n_rows > 0) {
     MR_HIP(hipMemsetAsync(c->row_cur.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
+    MR_HIP(hipMemsetAsync(c->row_nnz.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
-                  c->dense_div, c->force32, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr};
-    if (c->n_heavy > 0) {
-      hipLaunchKernelGGL(k_cooc_build<MR_COOC_NT>, dim3(c->n_heavy * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
+                  c->dense_div, c->force32, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
+                  c->row_nnz.p};
+    // heavy rows: >= 65536 listeners with u32 counters, then the rest with u16 pairs
+    const int n32 = c->n_heavy32, n16 = c->n_heavy - c->n_heavy32;
+    if (n32 > 0) {
+      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT, false>), dim3(n32 * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
+      MR_HIP(hipGetLastError());
+    }
+    if (n16 > 0) {
+      CoocParams hp = cp;
+      hp.rows = c->rows_order.p + n32;
+      if (hp.stamps) hp.stamps += (size_t)n32 * c->n_tiles * 8;
+      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT16, true>), dim3(n16 * c->n_tiles), dim3(MR_COOC_NT16),
+                         (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }
     if (c->n_light > 0) {

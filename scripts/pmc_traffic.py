@@ -14,7 +14,10 @@ import json
 import statistics
 import sys
 
+import os
+
 cfg, pat, out_path, dirs = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4:]
+ROUTE = os.environ.get("IBM_ROUTE")  # the ibm route the passes ran (bench.py checks it before using the file)
 if pat.startswith("step:"):
     parts = pat.split(":")
     n_steps = int(parts[1])
@@ -37,6 +40,7 @@ if pat.startswith("step:"):
            "dispatches": {c: len(v) for c, v in disp.items()}, "per_step": per_step,
            "fetch_bytes_corrected": fetch, "write_bytes": write, "traffic_bytes_per_launch": fetch + write,
            "traffic_unit": "bytes per step (bench's roofline for multi-kernel steps is per step)",
+           "ibm_route": ROUTE,
            "l2_hit_rate": (per_step["TCC_HIT_sum"] / (per_step["TCC_HIT_sum"] + per_step["TCC_MISS_sum"]))
            if "TCC_HIT_sum" in per_step else None,
            "traffic_note": "fetched = 2 x FETCH_SIZE (profiles/r02/c4/fetch_calibration.json) + WRITE_SIZE, "
