@@ -1568,7 +1568,8 @@ constexpr int kCoocCntBits = 17;
 // seg_len of a dense segment (counts of every song of the tile, u16 / u32)
 constexpr int kCoocDense16 = -1;
 constexpr int kCoocDense32 = -2;
-constexpr int kCoocDenseDiv = 3;  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
+constexpr int kCoocDenseDiv = 3;
+constexpr int kCoocBigRow = 4096;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
 constexpr int kCoocMaxTile = 1 << (32 - kCoocCntBits);
 
@@ -1978,14 +1979,15 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 // Co-listening index (ibm_route 2), built at the start of every ibm run: for
 // index row r (a test-visible song s2 = row_song[r] with train listeners) and
 // song tile t, the counts C[s2][s] = |L_tr(s2) ∩ L_tr(s)| (the distinct-user
-// numerator of MR:232-235) of every song s of the tile with C > 0, as packed
-// entries (tile-local s << kCoocCntBits) | C in song order. One workgroup per
-// (row, tile): u32 counters in LDS, the row's listeners walked over the
-// tile-major train CSR like the two-hop stage 2 (weight 1), then compacted by
-// wave ballots. The row's tiles reserve their segments from its pool range
-// (row_base[r], capacity = a bound on the row's non-zeros) with one atomic on
-// row_cur[r] each. Rows come sorted by listener count, heaviest first, and
-// blockIdx.x = row * n_tiles + tile, so the long walks start first.
+// numerator of MR:232-235) of every song s of the tile with C > 0: a sparse
+// segment of packed entries (tile-local s << kCoocCntBits) | C, or a dense one
+// (every song's count, u16 / u32) when a third of the tile is non-zero.
+// Heavy rows: one workgroup per row (k_cooc_build), its tiles in turn — LDS
+// counters, the row's listeners walked over the tile-major train CSR like the
+// two-hop stage 2 (weight 1), then the segment written at a running offset
+// from row_base[r] (the host's bound on the row's words). Light rows: one
+// workgroup per row with an LDS hash of its listeners' whole rows
+// (k_cooc_light). Rows come sorted by listener count, heaviest first.
 // ---------------------------------------------------------------------------
 struct CoocParams {
   int n_tr, n_rows, n_tiles, block_songs, song_lo, song_hi;
@@ -1995,7 +1997,6 @@ struct CoocParams {
   const int* trs_users;
   const int* row_song;           // [n_rows]
   const long long* row_base;     // [n_rows] first pool entry of the row
-  unsigned* row_cur;             // [n_rows] entries reserved so far (zeroed before the launch)
   unsigned* pool;
   long long* seg_off;            // [tile][row]
   int* seg_len;                  // [tile][row]
@@ -2008,12 +2009,22 @@ struct CoocParams {
   int force32;                   // 1: dense counts as u32 even below 65536 listeners (tests)
   long long* stamps;             // diagnostic build: [workgroup][8] s_memrealtime at phase ends
   unsigned* row_nnz;             // [n_rows] non-zero counts of the row over the shard (zeroed per run)
+  int n_big;                     // k_cooc_build: the first n_big rows of the launch one workgroup per
+                                 //   (row, tile), each tile's segment at row_base + tile * tcap
+  int tcap;                      //   (words per tile of those rows); the rest one workgroup per row
 };
 
 template <bool P16>
 __host__ __device__ inline int cooc_words(int bs) { return P16 ? (bs + 1) / 2 : bs; }
+// songs first touched during the walk (u16, tile-local): a sparse segment of
+// at most this many non-zeros is written from the list, without a scan of the
+// tile (sized so 4 / 2 workgroups of a 19,456-song tile still fit one CU)
 template <bool P16>
-__host__ __device__ inline int cooc_build_lds(int bs) { return align16(cooc_words<P16>(bs) * 4) + 16 * 4 + 16; }
+__host__ __device__ constexpr int cooc_list_cap() { return P16 ? 960 : 1984; }
+template <bool P16>
+__host__ __device__ inline int cooc_build_lds(int bs) {
+  return align16(cooc_words<P16>(bs) * 4) + 16 * 4 + 32 + cooc_list_cap<P16>() * 2;
+}
 
 // Light rows (k_cooc_light): an LDS hash table of packed slots
 // ((shard-local song + 1) << kLightCntBits) | count, at most kLightSlots;
@@ -2038,25 +2049,29 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
   const int bs = p.block_songs;
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
   int* s_scan = reinterpret_cast<int*>(smem_raw + align16(cooc_words<P16>(bs) * 4));
+  int* s_nz = s_scan + 16;
+  unsigned short* touched = reinterpret_cast<unsigned short*>(s_scan + 16 + 8);
+  constexpr int kCap = cooc_list_cap<P16>();
   auto count_of = [&](int i) -> unsigned {
     if constexpr (P16) return (cnt[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
     else return cnt[i];
   };
-  long long* s_base = reinterpret_cast<long long*>(s_scan + 16);
-  const int ri = blockIdx.x / p.n_tiles, tile = blockIdx.x - ri * p.n_tiles;
+  // big rows: one workgroup per (row, tile) at a fixed offset; the others:
+  // one workgroup per row, its tiles in turn at a running offset
+  const int nbt = p.n_big * p.n_tiles;
+  const bool big = (int)blockIdx.x < nbt;
+  const int ri = big ? (int)blockIdx.x / p.n_tiles : p.n_big + ((int)blockIdx.x - nbt);
   const int r = p.rows[ri];
+  const int t_begin = big ? (int)blockIdx.x - ri * p.n_tiles : 0;
+  const int t_end = big ? t_begin + 1 : p.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int blo = p.song_lo + tile * bs;
-  const int bw = min(p.song_hi, blo + bs) - blo;
   long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
   stamp_rt(sb, 0);
-  for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
-  __syncthreads();
-  stamp_rt(sb, 1);
   const int s2 = p.row_song[r];
   const long long a = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - a);
   const int* lst = p.trs_users + a;
+  const bool c16 = n < 65536 && !p.force32;
   constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
   auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
 #pragma unroll
@@ -2066,72 +2081,87 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
       q[j] = 1u;
     }
   };
-  walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
-                                         [&](unsigned x, unsigned) {
-                                           if constexpr (P16) atomicAdd(&cnt[x >> 1], 1u << ((x & 1) << 4));
-                                           else atomicAdd(&cnt[x], 1u);
-                                         });
-  __syncthreads();
-  stamp_rt(sb, 2);
-  // compaction: wave w owns songs [wb, we) (a multiple of 64 wide), counted by
-  // ballots, then written in song order at the wave's offset
-  const int q4 = (bw + NT - 1) / NT * 64;
-  const int wb = min(bw, w * q4), we = min(bw, wb + q4);
-  int nz = 0;
-  for (int i0 = wb; i0 < we; i0 += 64) {
-    const int i = i0 + lane;
-    nz += __popcll(__ballot(i < we && count_of(i) != 0u));
-  }
-  if (lane == 0) s_scan[w] = nz;
-  __syncthreads();
-  int base = 0, total = 0;
-#pragma unroll
-  for (int x = 0; x < NW; ++x) {
-    base += x < w ? s_scan[x] : 0;
-    total += s_scan[x];
-  }
-  // Dense segment when at least a third of the tile's songs are non-zero:
-  // every song's count as u16 (listener count < 65536: no count can exceed
-  // it) or u32, no index and no atomics on the consumer side. Reservations
-  // are whole 16-B words (dense segments are read by 16-B loads).
-  const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
-  const bool c16 = n < 65536 && !p.force32;
-  // (u32 dense: whole 32-B words, read 8 songs at a time)
-  const int words = dense ? (c16 ? ((bw + 1) / 2 + 3) & ~3 : (bw + 7) & ~7) : (total + 3) & ~3;
-  if (tid == 0) {
-    if (total) atomicAdd(&p.row_nnz[r], (unsigned)total);
-    const unsigned at = words ? atomicAdd(&p.row_cur[r], (unsigned)words) : 0u;
-    const long long off = p.row_base[r] + at;
-    p.seg_off[(size_t)tile * p.n_rows + r] = off;
-    p.seg_len[(size_t)tile * p.n_rows + r] = dense ? (c16 ? kCoocDense16 : kCoocDense32) : total;
-    s_base[0] = off;
-  }
-  __syncthreads();
-  stamp_rt(sb, 3);
-  if (sb && tid == 0) sb[6] = n;
-  unsigned* out = p.pool + s_base[0];
-  if (dense) {
-    if (c16) {
-      for (int i = tid; 2 * i < bw; i += NT) {
-        if constexpr (P16) out[i] = cnt[i];  // the LDS words are the u16 pairs already
-        else out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
-      }
-    } else {
-      for (int i = tid; i < bw; i += NT) out[i] = count_of(i);
-    }
-    stamp_rt(sb, 4);
-    if (sb && tid == 0) sb[5] = 1;  // dense
-    return;
-  }
+  // the row's tiles one after another: its segments are laid out in tile
+  // order from row_base[r] (no reservation atomics; the capacity bound holds)
+  long long off = p.row_base[r] + (long long)t_begin * p.tcap;  // (t_begin = 0 unless big)
+  unsigned row_nz = 0u;
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int i0 = wb; i0 < we; i0 += 64) {
-    const int i = i0 + lane;
-    const unsigned c = i < we ? count_of(i) : 0u;
-    const unsigned long long m = __ballot(c != 0u);
-    if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
-    base += __popcll(m);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int blo = p.song_lo + tile * bs;
+    const int bw = min(p.song_hi, blo + bs) - blo;
+    for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
+    if (tid == 0) *s_nz = 0;
+    __syncthreads();
+    walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
+                                           [&](unsigned x, unsigned) {
+                                             bool first;
+                                             if constexpr (P16) {
+                                               const unsigned sh = (x & 1) << 4;
+                                               first = ((atomicAdd(&cnt[x >> 1], 1u << sh) >> sh) & 0xffffu) == 0u;
+                                             } else {
+                                               first = atomicAdd(&cnt[x], 1u) == 0u;
+                                             }
+                                             if (first) {
+                                               const int k = atomicAdd(s_nz, 1);
+                                               if (k < kCap) touched[k] = (unsigned short)x;
+                                             }
+                                           });
+    __syncthreads();
+    const int total = *s_nz;
+    // Dense segment when at least a third of the tile's songs are non-zero:
+    // every song's count as u16 (listener count < 65536: no count can exceed
+    // it) or u32, no index and no atomics on the consumer side. Segments are
+    // whole 16-B words (32-B for u32 counts: read 8 songs at a time).
+    const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
+    const int words = dense ? (c16 ? ((bw + 1) / 2 + 3) & ~3 : (bw + 7) & ~7) : (total + 3) & ~3;
+    if (tid == 0) {
+      p.seg_off[(size_t)tile * p.n_rows + r] = off;
+      p.seg_len[(size_t)tile * p.n_rows + r] = dense ? (c16 ? kCoocDense16 : kCoocDense32) : total;
+    }
+    unsigned* out = p.pool + off;
+    if (dense) {
+      if (c16) {
+        for (int i = tid; 2 * i < bw; i += NT) {
+          if constexpr (P16) out[i] = cnt[i];  // the LDS words are the u16 pairs already
+          else out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
+        }
+      } else {
+        for (int i = tid; i < bw; i += NT) out[i] = count_of(i);
+      }
+    } else if (total <= kCap) {  // the touched list holds every non-zero song
+      for (int k = tid; k < total; k += NT) {
+        const unsigned x = touched[k];
+        out[k] = (x << kCoocCntBits) | count_of((int)x);
+      }
+    } else {  // song-ordered compaction: wave w owns songs [wb, we), offsets by ballots
+      const int q4 = (bw + NT - 1) / NT * 64;
+      const int wb = min(bw, w * q4), we = min(bw, wb + q4);
+      int nz = 0;
+      for (int i0 = wb; i0 < we; i0 += 64) {
+        const int i = i0 + lane;
+        nz += __popcll(__ballot(i < we && count_of(i) != 0u));
+      }
+      if (lane == 0) s_scan[w] = nz;
+      __syncthreads();
+      int base = 0;
+#pragma unroll
+      for (int x = 0; x < NW; ++x) base += x < w ? s_scan[x] : 0;
+      for (int i0 = wb; i0 < we; i0 += 64) {
+        const int i = i0 + lane;
+        const unsigned c = i < we ? count_of(i) : 0u;
+        const unsigned long long m = __ballot(c != 0u);
+        if (c) out[base + __popcll(m & below)] = ((unsigned)i << kCoocCntBits) | c;
+        base += __popcll(m);
+      }
+    }
+    off += words;
+    row_nz += (unsigned)total;
+    __syncthreads();  // the next tile rezeroes the counters
   }
-  stamp_rt(sb, 4);
+  if (tid == 0) {
+    if (row_nz) atomicAdd(&p.row_nnz[r], row_nz);
+    if (sb) { sb[4] = (long long)__builtin_amdgcn_s_memrealtime(); sb[5] = big; sb[6] = n; }
+  }
 }
 
 // Light index rows: one workgroup per row (instead of one per (row, tile)).
@@ -2486,12 +2516,13 @@ struct mr_ctx {
   ScoreKernel cooc_kernel = nullptr;
   DevBuf<int> row_song, te_row, seg_len;
   DevBuf<long long> row_base, seg_off;
-  DevBuf<unsigned> row_cur, pool;
+  DevBuf<unsigned> pool;
   DevBuf<unsigned> row_nnz;        // per run: each index row's non-zeros over the shard
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
+  int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
@@ -2509,7 +2540,7 @@ struct mr_ctx {
     stamps.release();
     flag.release();
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
-    row_cur.release(); pool.release();
+    pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     row_users.clear(); build_reads = 0;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -3045,7 +3076,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   std::vector<int64_t> row_base;
   std::vector<int32_t> heavy_rows, light_rows, row_slots;
   int dense_div = kCoocDenseDiv;
-  int n_heavy32 = 0;
+  int n_heavy32 = 0, n_big16 = 0, tcap16 = 0, tcap32 = 0;
   std::vector<int64_t> row_reads;
   int64_t pool_cap = 0;
   {
@@ -3121,6 +3152,21 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         return !MR_COOC_P16 || col_tr[row_song[r]] >= 65536;
       });
       for (int32_t r : heavy_rows) n_heavy32 += (!MR_COOC_P16 || col_tr[row_song[r]] >= 65536) ? 1 : 0;
+      // Big rows (>= kCoocBigRow listeners, and every u32 row): one workgroup
+      // per (row, tile), each tile a fixed slot of tcap words (the larger of a
+      // dense segment and the longest sparse one), so the row's tiles run in
+      // parallel. Rows are heaviest first, so the big rows of each kind lead.
+      const int sparse_max = dense_div > 0 ? (bs + dense_div - 1) / dense_div : bs;
+      tcap32 = (std::max(sparse_max, bs) + 7) & ~7;
+      tcap16 = cooc_dense32_opt() ? tcap32 : (std::max(sparse_max, (bs + 1) / 2) + 7) & ~7;
+      n_big16 = 0;
+      for (size_t i = n_heavy32; i < heavy_rows.size(); ++i) {
+        if (col_tr[row_song[heavy_rows[i]]] < kCoocBigRow) break;
+        n_big16++;
+      }
+      for (size_t i = 0; i < heavy_rows.size(); ++i)
+        if ((int)i < n_heavy32 + n_big16)
+          row_base[heavy_rows[i]] = (int64_t)n_tiles * ((int)i < n_heavy32 ? tcap32 : tcap16);
       pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
       row_base[nr] = pool_cap;
       size_t free_b = 0, total_b = 0;
@@ -3186,7 +3232,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_upload(c->row_song, row_song.data(), nr, st))) return rc;
     if ((rc = dev_upload(c->te_row, te_row.data(), te_row.size(), st))) return rc;
     if ((rc = dev_upload(c->row_base, reinterpret_cast<const long long*>(row_base.data()), nr + 1, st))) return rc;
-    if ((rc = dev_alloc(c->row_cur, nr))) return rc;
     if ((rc = dev_alloc(c->row_nnz, nr))) return rc;
     if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
@@ -3273,6 +3318,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     for (size_t i = 0; i < (size_t)d->te_off[n_te]; ++i)
       if (te_row[i] >= 0) c->row_users[te_row[i]]++;
     c->n_heavy32 = n_heavy32;
+    c->n_big16 = n_big16;
+    c->tcap16 = tcap16;
+    c->tcap32 = tcap32;
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
@@ -3417,24 +3465,30 @@ int run_cooc(mr_ctx* c) {
     MR_HIP(hipEventRecord(ev[0], st));
   }
   if (c->n_rows > 0) {
-    MR_HIP(hipMemsetAsync(c->row_cur.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
     MR_HIP(hipMemsetAsync(c->row_nnz.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
-                  c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->row_cur.p, c->pool.p,
+                  c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
                   c->dense_div, c->force32, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
                   c->row_nnz.p};
     // heavy rows: >= 65536 listeners with u32 counters, then the rest with u16 pairs
     const int n32 = c->n_heavy32, n16 = c->n_heavy - c->n_heavy32;
-    if (n32 > 0) {
-      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT, false>), dim3(n32 * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st, cp);
+    if (n32 > 0) {  // all big: one workgroup per (row, tile)
+      CoocParams hp = cp;
+      hp.n_big = n32;
+      hp.tcap = c->tcap32;
+      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT, false>), dim3(n32 * c->n_tiles), dim3(MR_COOC_NT), c->cooc_lds, st,
+                         hp);
       MR_HIP(hipGetLastError());
     }
     if (n16 > 0) {
       CoocParams hp = cp;
       hp.rows = c->rows_order.p + n32;
+      hp.n_big = c->n_big16;
+      hp.tcap = c->tcap16;
       if (hp.stamps) hp.stamps += (size_t)n32 * c->n_tiles * 8;
-      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT16, true>), dim3(n16 * c->n_tiles), dim3(MR_COOC_NT16),
+      hipLaunchKernelGGL((k_cooc_build<MR_COOC_NT16, true>), dim3(c->n_big16 * c->n_tiles + n16 - c->n_big16),
+                         dim3(MR_COOC_NT16),
                          (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }

@@ -1,8 +1,8 @@
-"""Per-workgroup phase stamps of the co-listening index build (k_cooc_build,
-heavy rows, one workgroup per (row, tile)) in the diagnostic build
-libmr_engine_stamps.so. Usage: python scripts/cooc_stamps.py [N_TRAIN N_TEST]
-Phases (s_memrealtime, 100 MHz): zero the counters | walk the listeners |
-count + reserve | write the segment."""
+"""Per-workgroup times of the co-listening index build (k_cooc_build: big
+rows one workgroup per (row, tile), the other heavy rows one per row, its
+tiles in turn) in the diagnostic build libmr_engine_stamps.so
+(s_memrealtime, 100 MHz, at the workgroup's start and end).
+Usage: python scripts/cooc_stamps.py [N_TRAIN N_TEST]"""
 import os
 import sys
 
@@ -23,26 +23,21 @@ with Engine(ds, topk=10, dense=False, ibm_route="cooc") as e:
     e.sync()
     off = e.n_tiles * (max(e.batch, min(n_te, 65528)) + 8) * 32
     total = off + 8 * e.n_tiles * e.cooc_rows
+    e_tiles = e.n_tiles
     buf = np.zeros(total, dtype=np.int64)
     assert e._L.mr_debug_stamps(e._h, buf.ctypes.data, buf.size) == 0
 b = buf[off:].reshape(-1, 8)
 b = b[b[:, 0] != 0]
-us = (b[:, :5] - b[:, :1]).astype(np.float64) * 10.0 / 1e3  # from WG start, us
+dur = (b[:, 4] - b[:, 0]).astype(np.float64) * 10.0 / 1e3  # us per workgroup
 n = b[:, 6]
-dense = b[:, 5] == 1
+big = b[:, 5] == 1
 span = (b[:, 4].max() - b[:, 0].min()) * 10.0 / 1e3
-dur = us[:, 4]
-print(f"{n_tr}/{n_te}: build WGs {len(b)} (dense segments {dense.mean():.2f}), kernel span {span / 1e3:.2f} ms, "
-      f"sum(WG time)/512 = {dur.sum() / 512 / 1e3:.2f} ms")
-for name, a, c in (("zero", 0, 1), ("walk", 1, 2), ("count", 2, 3), ("write", 3, 4), ("total", 0, 4)):
-    d = us[:, c] - us[:, a]
-    print(f"  {name:6s} us med {np.median(d):8.1f} p90 {np.percentile(d, 90):8.1f} max {d.max():9.1f} "
-          f"share {d.sum() / dur.sum():.3f}")
+print(f"{n_tr}/{n_te}: workgroups {len(b)} ({big.sum()} per (row, tile), {(~big).sum()} per row), "
+      f"kernel span {span / 1e3:.2f} ms, sum(WG time)/1024 = {dur.sum() / 1024 / 1e3:.2f} ms, longest {dur.max() / 1e3:.2f} ms")
 edges = [0, 256, 1024, 4096, 16384, 65536, 1 << 30]
-for lo, hi in zip(edges[:-1], edges[1:]):
-    m = (n >= lo) & (n < hi)
-    if not m.any():
-        continue
-    w = us[m, 2] - us[m, 1]
-    print(f"  listeners [{lo},{hi}): WGs {m.sum():7d} walk med {np.median(w):8.1f} us, total med "
-          f"{np.median(dur[m]):8.1f} us, share of WG time {dur[m].sum() / dur.sum():.3f}")
+for kind, m0, tiles in (("per row", ~big, e_tiles), ("per (row, tile)", big, 1)):
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        m = m0 & (n >= lo) & (n < hi)
+        if m.any():
+            print(f"  {kind:15s} listeners [{lo},{hi}): WGs {m.sum():7d} time med {np.median(dur[m]):9.1f} us, "
+                  f"per listener-tile {np.median(dur[m] / (n[m] * tiles)) * 1e3:7.2f} ns, share {dur[m].sum() / dur.sum():.3f}")
