@@ -103,6 +103,13 @@ case ",$STEPS," in *,c4map,*)
     MR_WIDE_MAP=$m run c4map_$m 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4map_$m" -o p -- python3 "$ROOT/bench.py" --config c4 --steps 5 --warmup 2 --no-e2e --no-cpu-baseline --no-north-star
   done ;;
 esac
+# any config per ibm route under rocprofv3 stats: CFG=c3 ROUTES="cooc two_hop"
+case ",$STEPS," in *,cfgroute,*)
+  export TMPDIR=/tmp
+  for r in ${ROUTES:-cooc two_hop}; do
+    run ${CFG}_$r 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${CFG}_$r" -o p -- python3 "$ROOT/bench.py" --config $CFG --steps ${CSTEPS:-20} --warmup 3 --no-e2e --no-cpu-baseline --no-north-star --ibm-route $r
+  done ;;
+esac
 case ",$STEPS," in *,profc4cooc,*)
   export TMPDIR=/tmp
   run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;
