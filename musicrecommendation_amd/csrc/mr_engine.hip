@@ -2645,6 +2645,28 @@ int cooc_dense32_opt() {
   return e && std::atoi(e) == 1 ? 1 : 0;
 }
 
+// Auto route rule: the co-listening route when its estimated device time is
+// below the two-hop route's. Per-unit costs fitted on one MI355X
+// (profiles/r03/cooc/route_model.txt): two-hop 5.75 ps per estimated
+// (tile, test user, neighbour) visit, neighbours estimated by Σ_{s2∈T(u)}
+// c_tr(s2) capped at n_tr (C4 286 ms of stage-2 time); co-listening build
+// 35 ps per heavy (row, tile, listener) visit and 12.8 ps per light-row entry,
+// scoring 0.49 ps per estimated consumed entry (bound of the row's non-zeros),
+// plus a latency floor of 28 ns per light row and 24 ns per heavy (row, tile)
+// workgroup (C3: 0.30 ms for 10.7k light rows). C3 -> two-hop (0.77 vs 0.38 ms
+// estimated; 1.53 vs 1.09 measured), C4 / C5 -> co-listening (62 vs 286 ms,
+// 28 vs 58 ms estimated).
+bool cooc_pays(double v_est, double e_est, const std::vector<int64_t>& bound, const std::vector<int64_t>& reads,
+               const std::vector<int32_t>& row_song, const std::vector<int32_t>& col_tr, int n_tiles) {
+  double build = 0.0;
+  for (size_t r = 0; r < row_song.size(); ++r) {
+    const double c = col_tr[row_song[r]];
+    if (bound[r] <= kLightSlots / 2 && c <= kLightCntMask) build += 12.8e-12 * (double)(reads[r] - c) + 28e-9;
+    else build += n_tiles * (35e-12 * c + 24e-9);
+  }
+  return build + 0.49e-12 * e_est < 5.75e-12 * v_est;
+}
+
 int wide_map_opt() {
   static const int m = [] {
     const char* e = std::getenv("MR_WIDE_MAP");
@@ -3125,7 +3147,24 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           row_base[r] = std::min<int64_t>(sum, width);  // the row's non-zeros: its sparse bound
         }
       }, 256);
+      // auto: the cost model of cooc_pays (the rows' bounds = sparse entry bounds here)
+      if (c->opt.ibm_route == 0) {
+        double e_est = 0.0;
+        for (int64_t i = 0; i < d->te_off[n_te]; ++i)
+          if (te_row[i] >= 0) e_est += (double)row_base[te_row[i]];
+        double v_est = 0.0;
+        for (int u = 0; u < n_te; ++u) {
+          double sc = 0.0;
+          for (int64_t i = d->te_off[u]; i < d->te_off[u + 1]; ++i) sc += col_tr[d->te_songs[i]];
+          v_est += std::min<double>(sc, n_tr);
+        }
+        if (!cooc_pays(v_est * n_tiles, e_est, row_base, row_reads, row_song, col_tr, n_tiles))
+          why = "a cheaper estimate than the two-hop route (auto)";
+      }
+    }
+    if (!why && c->opt.ibm_route != 1) {
       // light rows (k_cooc_light): the bound fits half the hash slots
+      const int64_t nr = (int64_t)row_song.size();
       const bool light_ok = width <= kLightMaxWidth && n_tiles <= kLightMaxTiles && cooc_light_opt();
       dense_div = cooc_dense_div_opt();
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
