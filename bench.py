@@ -371,18 +371,21 @@ def north_star(args, world: int, rank: int, local: int):
     partitions by song-id range across the 8 GPUs ... with a single RCCL
     all-gather of per-test-user partial scores"): C4 = the full Taste-Profile
     shape (1,009,318 train / 10,000 test / 384,546 songs, top-10), strong
-    scaling over the fixed test set in the 2-D layout of sharding.ShardScorer —
-    G_s song shards (2 when N is even, else N) x N / G_s test-user blocks; the
-    song shards of a block exchange their top-k record blocks with ONE
-    all-gather (RCCL) and merge them on the device (distributed.scala:477-479's
-    song partition, :468-470's user partition). Every rank runs this; returns
-    the block for rank 0's line (None elsewhere)."""
+    scaling over the fixed test set: N song shards (sharding.ShardScorer with
+    G_s = N, G_u = 1), each an equal whole number of tiles
+    (mr_shard_tile_songs_n: C4 over 8 shards = 24 tiles, 3 per GPU); every
+    rank scores all test users over its songs — with the co-listening route
+    its index holds only its songs' columns, so nothing is built twice (user
+    blocks would each rebuild the popular rows) — and the shards exchange
+    their top-k record blocks with ONE all-gather (RCCL) and merge them on the
+    device (distributed.scala:477-479's song partition). Every rank runs this;
+    returns the block for rank 0's line (None elsewhere)."""
     from musicrecommendation_amd.sharding import ShardScorer
 
     t0 = time.perf_counter()
     full = synth.config("c4").dataset()
     gen_s = time.perf_counter() - t0
-    gs = 1 if world == 1 else (2 if world % 2 == 0 else world)
+    gs = world
     t0 = time.perf_counter()
     scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32",
                          ibm_route=args.ibm_route)
@@ -420,6 +423,8 @@ def north_star(args, world: int, rank: int, local: int):
             "workload": f"c4: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} {full.n_train} train / "
                         f"{full.n_test} test / {full.n_songs} songs, top-10 only",
             "layout": f"songs{scorer.gs}xusers{scorer.gu}", "song_shards": scorer.gs, "user_blocks": scorer.gu,
+            "ibm_route": scorer.engine.ibm_route, "tiles_per_rank": scorer.engine.n_tiles,
+            "songs_per_rank": scorer.engine.width,
             "value": pairs * args.ns_steps / step_s, "unit": "pairs/s", "scaling": "strong",
             "pairs_per_step": pairs, "steps": args.ns_steps, "warmup": args.ns_warmup,
             "ms_per_step": ms,  # slowest rank: max over ranks of the barrier-bracketed window

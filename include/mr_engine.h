@@ -186,6 +186,14 @@ int mr_cooc_stats(mr_ctx* ctx, int64_t* index_nnz, int64_t* consumed, int64_t* b
 int mr_shard_tile_songs(const mr_options* opt, int32_t n_train_users, int32_t n_test_users,
                         int32_t* tile_songs);
 
+/* The same for a layout of n_shards song shards over n_songs songs: the tile
+ * narrowed so that the shards hold the same whole number of tiles (the tile
+ * count rounded up to a multiple of n_shards; = mr_shard_tile_songs for one
+ * shard or an explicit opt->block_songs). mr_group_load and the per-process
+ * layouts (sharding.ShardScorer) cut their shards with it. */
+int mr_shard_tile_songs_n(const mr_options* opt, int32_t n_train_users, int32_t n_test_users, int32_t n_songs,
+                          int32_t n_shards, int32_t* tile_songs);
+
 /*
  * Score every (test user, song) pair of the shard for `model`, leaving the
  * results in device buffers (asynchronous on the context stream):

@@ -130,6 +130,7 @@ SIGNATURES = {
     "mr_route_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int64)]),
     "mr_cooc_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "mr_shard_tile_songs": (c_int, [POINTER(MrOptions), c_int32, c_int32, POINTER(c_int32)]),
+    "mr_shard_tile_songs_n": (c_int, [POINTER(MrOptions), c_int32, c_int32, c_int32, c_int32, POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),
     "mr_sync": (c_int, [c_void_p]),
     "mr_graph_capture": (c_int, [c_void_p, c_int, c_int32]),

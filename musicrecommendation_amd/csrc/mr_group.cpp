@@ -476,7 +476,8 @@ int mr_group_load(mr_group* g, const mr_dataset* d) {
     x.stream = nullptr;
   }
   int tile = 0;  // the wide shape's tile when the contexts will use it (mr_shard_tile_songs)
-  if (int rc = mr_shard_tile_songs(&g->opt, d->n_train_users, d->n_test_users / g->gu(), &tile)) return rc;
+  if (int rc = mr_shard_tile_songs_n(&g->opt, d->n_train_users, d->n_test_users / g->gu(), d->n_songs, g->gs(), &tile))
+    return rc;
   const std::vector<int> sb = song_bounds(d, g->gs(), tile);
   // Per user block: a view of the dataset over its test users (te_off rebased).
   std::vector<std::vector<int64_t>> te_off(g->gu());

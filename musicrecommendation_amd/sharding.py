@@ -57,9 +57,11 @@ def song_shards(ds: Dataset, n_shards: int, tile: int = 0) -> List[Tuple[int, in
 
 
 def shard_tile(n_train: int, n_test: int, *, topk: int = 10, stage1: str = "auto", block_songs: int = 0,
-               stage1_chunk: int = 0) -> int:
+               stage1_chunk: int = 0, n_songs: int = 0, n_shards: int = 1) -> int:
     """The wide shape's song tile for a context scoring n_test x n_train users
-    with these options (mr_shard_tile_songs), 0 when it would use another shape."""
+    with these options (mr_shard_tile_songs), 0 when it would use another shape;
+    with n_songs and n_shards > 1, narrowed so the shards hold equal whole
+    numbers of tiles (mr_shard_tile_songs_n)."""
     import ctypes
 
     from . import _lib
@@ -72,8 +74,12 @@ def shard_tile(n_train: int, n_test: int, *, topk: int = 10, stage1: str = "auto
     opt.stage1 = _lib.STAGE1[stage1]
     opt.stage1_chunk = stage1_chunk
     out = ctypes.c_int32()
-    _lib.check(L.mr_shard_tile_songs(ctypes.byref(opt), int(n_train), int(n_test), ctypes.byref(out)),
-               "mr_shard_tile_songs")
+    if n_songs > 0 and n_shards > 1:
+        _lib.check(L.mr_shard_tile_songs_n(ctypes.byref(opt), int(n_train), int(n_test), int(n_songs), int(n_shards),
+                                           ctypes.byref(out)), "mr_shard_tile_songs_n")
+    else:
+        _lib.check(L.mr_shard_tile_songs(ctypes.byref(opt), int(n_train), int(n_test), ctypes.byref(out)),
+                   "mr_shard_tile_songs")
     return out.value
 
 
@@ -186,7 +192,8 @@ class ShardScorer:
         self.rank, self.world = rank, world
         self.block, self.shard = rank // self.gs, rank % self.gs
         self.user_lo, self.user_hi = user_blocks(ds.n_test, self.gu)[self.block]
-        tile = shard_tile(ds.n_train, ds.n_test // self.gu, topk=topk, stage1=stage1, block_songs=block_songs)
+        tile = shard_tile(ds.n_train, ds.n_test // self.gu, topk=topk, stage1=stage1, block_songs=block_songs,
+                          n_songs=ds.n_songs, n_shards=self.gs)
         self.song_lo, self.song_hi = song_shards(ds, self.gs, tile)[self.shard]
         self.full = ds
         self.ds = ds if self.gu == 1 else ds.subset_test_users(self.user_lo, self.user_hi)
