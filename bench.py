@@ -232,7 +232,8 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     full = trip.dataset()
     gs, gu = layout_2d(world, song_groups_for(args, world))
     a, b = user_blocks(full.n_test, gu)[rank // gs]
-    lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu))[rank % gs]
+    lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu, n_songs=full.n_songs,
+                                              n_shards=gs))[rank % gs]
     ds = full if gu == 1 else full.subset_test_users(a, b)
     eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi, ibm_route=args.ibm_route)
     ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),

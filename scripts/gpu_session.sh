@@ -110,6 +110,8 @@ case ",$STEPS," in *,cfgroute,*)
     run ${CFG}_$r 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${CFG}_$r" -o p -- python3 "$ROOT/bench.py" --config $CFG --steps ${CSTEPS:-20} --warmup 3 --no-e2e --no-cpu-baseline --no-north-star --ibm-route $r
   done ;;
 esac
+# per-rank device time of C4 layouts, one rank at a time on this GPU: LAYOUTS="1x1,2x1,4x1,8x1"
+case ",$STEPS," in *,layouts,*) run layouts 900 python -u scripts/layout_probe.py ibm ${LAYOUTS:-1x1,2x1,4x1,8x1,2x4} ;; esac
 case ",$STEPS," in *,profc4cooc,*)
   export TMPDIR=/tmp
   run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;

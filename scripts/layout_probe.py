@@ -31,20 +31,22 @@ def main():
     base = None
     for gs, gu in layouts:
         t0 = time.time()
-        shards = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu) if tiled else 0)
+        tile = shard_tile(full.n_train, full.n_test // gu, n_songs=full.n_songs, n_shards=gs) if tiled else 0
+        shards = song_shards(full, gs, tile)
         blocks = user_blocks(full.n_test, gu)
         ranks = []
         for r in range(gs * gu):
             (a, b), (lo, hi) = blocks[r // gs], shards[r % gs]
             ds = full if gu == 1 else full.subset_test_users(a, b)
-            with Engine(ds, topk=10, dense=False, song_lo=lo, song_hi=hi) as e:
+            with Engine(ds, topk=10, dense=False, song_lo=lo, song_hi=hi,
+                        ibm_route=os.environ.get("MR_PROBE_ROUTE", "auto")) as e:
                 e.run(model)
                 e.sync()
                 e.timing_begin()
                 e.run(model)
                 _n, ms = e.timing_end()
                 ranks.append({"rank": r, "users": [a, b], "songs": [lo, hi], "n_tiles": e.n_tiles,
-                              "batch": e.batch, "device_ms": ms})
+                              "batch": e.batch, "ibm_route": e.ibm_route, "device_ms": ms})
         worst = max(x["device_ms"] for x in ranks)
         if (gs, gu) == (1, 1):
             base = worst

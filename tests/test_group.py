@@ -89,6 +89,12 @@ def test_shard_tile_follows_the_shape_rule():
     assert shard_tile(1_009_318, 10_000, topk=17) == 0
     with pytest.raises(_lib.EngineError):
         shard_tile(10, 0)
+    # song shards: the tile count rounded up to a multiple of the shard count
+    # (C4 over 8 shards: 24 tiles of 16,128, 3 per shard; 2 and 4 shards keep 20)
+    assert shard_tile(1_009_318, 10_000, n_songs=384_546, n_shards=8) == 16_128
+    assert shard_tile(1_009_318, 10_000, n_songs=384_546, n_shards=2) == 19_456
+    assert shard_tile(1_009_318, 10_000, n_songs=384_546, n_shards=4) == 19_456
+    assert shard_tile(1_009_318, 10_000, n_songs=384_546, n_shards=8, block_songs=8192) == 8192
 
 
 def test_group_without_gpu_fails_cleanly():
@@ -118,7 +124,8 @@ def test_copy_group_equals_one_context(layout):
                 ref[model] = (e.dense(), *e.topk())
         with Group(ds, song_shards=gs, user_blocks=gu, out_dtype="f64", topk=7) as g:
             assert g.transport == "copy" and len(g.layout) == gs * gu
-            shards = song_shards(ds, gs, shard_tile(ds.n_train, ds.n_test // gu, topk=7))
+            shards = song_shards(ds, gs, shard_tile(ds.n_train, ds.n_test // gu, topk=7, n_songs=ds.n_songs,
+                                                    n_shards=gs))
             for i, (slo, shi, ulo, uhi, dev) in enumerate(g.layout):
                 assert (slo, shi) == shards[i % gs] and dev == 0
             for model in ("ibm", "ubm"):
@@ -209,7 +216,8 @@ def test_c3_song_sharded_group_equals_one_context():
             e.run(model)
             ref[model] = (e.dense(), e.topk()[0], e.topk()[2])
     with Group(ds, song_shards=2, out_dtype="f32", topk=10) as g:
-        assert [(lo, hi) for lo, hi, *_ in g.layout] == song_shards(ds, 2, shard_tile(ds.n_train, ds.n_test))
+        assert [(lo, hi) for lo, hi, *_ in g.layout] == song_shards(
+            ds, 2, shard_tile(ds.n_train, ds.n_test, n_songs=ds.n_songs, n_shards=2))
         for model in ("ubm", "ibm"):
             g.run(model)
             songs, _scores, keys = g.topk()
