@@ -2036,8 +2036,13 @@ constexpr int kLightSlots = 32768;
 constexpr int kLightMaxTiles = 256;
 constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
 constexpr int kLightNT = 1024;
+// light rows of at most kLightSmallSlots slots: 256-thread workgroups with a
+// 16 KiB table (7 per CU instead of 1: the rows are latency-bound)
+constexpr int kLightSmallSlots = 4096;
+constexpr int kLightSmallNT = 256;
+template <int NT, int SMAX>
 __host__ __device__ inline int cooc_light_lds() {
-  return kLightSlots * 4 + 2 * kLightMaxTiles * 4 + kLightNT * 12 + 16 * 4 + 16;
+  return SMAX * 4 + 2 * kLightMaxTiles * 4 + NT * 12 + 16 * 4 + 16;
 }
 
 // P16: two u16 counters per LDS word (rows with < 65536 listeners: half the
@@ -2171,11 +2176,11 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
 // counts, their prefix -> the row's segment of every tile (seg_off / seg_len,
 // empty tiles included), entries placed by LDS cursors (order inside a
 // segment is arbitrary; the consumer's sums are order-free).
-__global__ __launch_bounds__(kLightNT) void k_cooc_light(CoocParams p) {
-  constexpr int NT = kLightNT;
+template <int NT, int SMAX>
+__global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   unsigned* tab = reinterpret_cast<unsigned*>(smem_raw);
-  int* tcnt = reinterpret_cast<int*>(tab + kLightSlots);
+  int* tcnt = reinterpret_cast<int*>(tab + SMAX);
   int* tpos = tcnt + kLightMaxTiles;
   long long* m_a = reinterpret_cast<long long*>(tpos + kLightMaxTiles);
   int* m_pre = reinterpret_cast<int*>(m_a + NT);
@@ -2521,6 +2526,7 @@ struct mr_ctx {
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
+  int n_light_small = 0;           // the last light rows: <= kLightSmallSlots hash slots
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
@@ -2543,7 +2549,7 @@ struct mr_ctx {
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     row_users.clear(); build_reads = 0;
-    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = n_light_small = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -3275,6 +3281,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
+    // heavy rows, then light rows with large tables, then the small-table ones
+    std::stable_partition(light_rows.begin(), light_rows.end(), [&](int32_t r) { return row_slots[r] > kLightSmallSlots; });
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
@@ -3363,8 +3371,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
-    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               cooc_light_lds()));
+    c->n_light_small = 0;
+    for (int32_t r : light_rows) c->n_light_small += row_slots[r] <= kLightSmallSlots ? 1 : 0;
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightNT, kLightSlots>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, cooc_light_lds<kLightNT, kLightSlots>()));
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightSmallNT, kLightSmallSlots>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               cooc_light_lds<kLightSmallNT, kLightSmallSlots>()));
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3545,10 +3558,20 @@ int run_cooc(mr_ctx* c) {
                          (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }
-    if (c->n_light > 0) {
+    const int nl_big = c->n_light - c->n_light_small;
+    if (nl_big > 0) {
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + c->n_heavy;
-      hipLaunchKernelGGL(k_cooc_light, dim3(c->n_light), dim3(kLightNT), (size_t)cooc_light_lds(), st, lp);
+      const size_t lds = (size_t)cooc_light_lds<kLightNT, kLightSlots>();
+      hipLaunchKernelGGL((k_cooc_light<kLightNT, kLightSlots>), dim3(nl_big), dim3(kLightNT), lds, st, lp);
+      MR_HIP(hipGetLastError());
+    }
+    if (c->n_light_small > 0) {
+      CoocParams lp = cp;
+      lp.rows = c->rows_order.p + c->n_heavy + nl_big;
+      const size_t lds = (size_t)cooc_light_lds<kLightSmallNT, kLightSmallSlots>();
+      hipLaunchKernelGGL((k_cooc_light<kLightSmallNT, kLightSmallSlots>), dim3(c->n_light_small), dim3(kLightSmallNT),
+                         lds, st, lp);
       MR_HIP(hipGetLastError());
     }
   }
