@@ -2037,9 +2037,15 @@ constexpr int kLightMaxTiles = 256;
 constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
 constexpr int kLightNT = 1024;
 // light rows of at most kLightSmallSlots slots: 256-thread workgroups with a
-// 16 KiB table (7 per CU instead of 1: the rows are latency-bound)
+// 16 KiB table (7 per CU instead of 1: the rows are latency-bound); up to
+// kLightMidSlots: 512-thread workgroups with 32 KiB (4 per CU)
 constexpr int kLightSmallSlots = 4096;
 constexpr int kLightSmallNT = 256;
+constexpr int kLightMidSlots = 8192;
+constexpr int kLightMidNT = 512;
+// a table of S slots holds a row whose entry bound is at most S * 4/5 (the
+// bound counts every listener's songs; the distinct ones are far fewer)
+__host__ __device__ constexpr long long light_bound_max(long long slots) { return slots * 4 / 5; }
 template <int NT, int SMAX>
 __host__ __device__ inline int cooc_light_lds() {
   return SMAX * 4 + 2 * kLightMaxTiles * 4 + NT * 12 + 16 * 4 + 16;
@@ -2527,6 +2533,7 @@ struct mr_ctx {
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
   int n_light_small = 0;           // the last light rows: <= kLightSmallSlots hash slots
+  int n_light_mid = 0;             // before them: <= kLightMidSlots
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
@@ -2549,7 +2556,7 @@ struct mr_ctx {
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     row_users.clear(); build_reads = 0;
-    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = n_light_small = 0;
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = n_light_small = n_light_mid = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -2667,7 +2674,7 @@ bool cooc_pays(double v_est, double e_est, const std::vector<int64_t>& bound, co
   double build = 0.0;
   for (size_t r = 0; r < row_song.size(); ++r) {
     const double c = col_tr[row_song[r]];
-    if (bound[r] <= kLightSlots / 2 && c <= kLightCntMask) build += 12.8e-12 * (double)(reads[r] - c) + 28e-9;
+    if (bound[r] <= light_bound_max(kLightSlots) && c <= kLightCntMask) build += 12.8e-12 * (double)(reads[r] - c) + 28e-9;
     else build += n_tiles * (35e-12 * c + 24e-9);
   }
   return build + 0.49e-12 * e_est < 5.75e-12 * v_est;
@@ -3175,9 +3182,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       dense_div = cooc_dense_div_opt();
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
-        if (light_ok && row_base[r] <= kLightSlots / 2 && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
+        if (light_ok && row_base[r] <= light_bound_max(kLightSlots) && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
           int sl = 1024;
-          while (sl < 2 * row_base[r]) sl <<= 1;
+          while (light_bound_max(sl) < row_base[r]) sl <<= 1;
           row_slots[r] = sl;
           light_rows.push_back((int32_t)r);
           row_base[r] = (row_base[r] + 3) & ~(int64_t)3;
@@ -3283,6 +3290,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
     // heavy rows, then light rows with large tables, then the small-table ones
     std::stable_partition(light_rows.begin(), light_rows.end(), [&](int32_t r) { return row_slots[r] > kLightSmallSlots; });
+    std::stable_partition(light_rows.begin(), light_rows.end(), [&](int32_t r) { return row_slots[r] > kLightMidSlots; });
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
@@ -3371,10 +3379,15 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
-    c->n_light_small = 0;
-    for (int32_t r : light_rows) c->n_light_small += row_slots[r] <= kLightSmallSlots ? 1 : 0;
+    c->n_light_small = c->n_light_mid = 0;
+    for (int32_t r : light_rows) {
+      c->n_light_small += row_slots[r] <= kLightSmallSlots ? 1 : 0;
+      c->n_light_mid += (row_slots[r] > kLightSmallSlots && row_slots[r] <= kLightMidSlots) ? 1 : 0;
+    }
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightNT, kLightSlots>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, cooc_light_lds<kLightNT, kLightSlots>()));
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightMidNT, kLightMidSlots>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, cooc_light_lds<kLightMidNT, kLightMidSlots>()));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightSmallNT, kLightSmallSlots>,
                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                cooc_light_lds<kLightSmallNT, kLightSmallSlots>()));
@@ -3558,7 +3571,7 @@ int run_cooc(mr_ctx* c) {
                          (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }
-    const int nl_big = c->n_light - c->n_light_small;
+    const int nl_big = c->n_light - c->n_light_small - c->n_light_mid;
     if (nl_big > 0) {
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + c->n_heavy;
@@ -3566,9 +3579,17 @@ int run_cooc(mr_ctx* c) {
       hipLaunchKernelGGL((k_cooc_light<kLightNT, kLightSlots>), dim3(nl_big), dim3(kLightNT), lds, st, lp);
       MR_HIP(hipGetLastError());
     }
-    if (c->n_light_small > 0) {
+    if (c->n_light_mid > 0) {
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + c->n_heavy + nl_big;
+      const size_t lds = (size_t)cooc_light_lds<kLightMidNT, kLightMidSlots>();
+      hipLaunchKernelGGL((k_cooc_light<kLightMidNT, kLightMidSlots>), dim3(c->n_light_mid), dim3(kLightMidNT),
+                         lds, st, lp);
+      MR_HIP(hipGetLastError());
+    }
+    if (c->n_light_small > 0) {
+      CoocParams lp = cp;
+      lp.rows = c->rows_order.p + c->n_heavy + nl_big + c->n_light_mid;
       const size_t lds = (size_t)cooc_light_lds<kLightSmallNT, kLightSmallSlots>();
       hipLaunchKernelGGL((k_cooc_light<kLightSmallNT, kLightSmallSlots>), dim3(c->n_light_small), dim3(kLightSmallNT),
                          lds, st, lp);
