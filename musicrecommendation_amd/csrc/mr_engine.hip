@@ -2035,14 +2035,12 @@ constexpr unsigned kLightCntMask = (1u << kLightCntBits) - 1u;
 constexpr int kLightSlots = 32768;
 constexpr int kLightMaxTiles = 256;
 constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
-constexpr int kLightNT = 1024;
-// light rows of at most kLightSmallSlots slots: 256-thread workgroups with a
-// 16 KiB table (7 per CU instead of 1: the rows are latency-bound); up to
-// kLightMidSlots: 512-thread workgroups with 32 KiB (4 per CU)
-constexpr int kLightSmallSlots = 4096;
-constexpr int kLightSmallNT = 256;
-constexpr int kLightMidSlots = 8192;
-constexpr int kLightMidNT = 512;
+// Light rows run in the smallest of four table sizes that holds them (the
+// rows are latency-bound, so smaller tables = more workgroups per CU):
+// 4096 slots / 256 threads (7 per CU), 8192 / 512 (4), 16384 / 512 (2),
+// 32768 / 1024 (1). Tier 0 is the largest (launched first).
+constexpr int kLightTiers = 4;
+__host__ __device__ constexpr int light_tier_slots(int t) { return 32768 >> t; }
 // a table of S slots holds a row whose entry bound is at most S * 4/5 (the
 // bound counts every listener's songs; the distinct ones are far fewer)
 __host__ __device__ constexpr long long light_bound_max(long long slots) { return slots * 4 / 5; }
@@ -2284,6 +2282,36 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
       const int pos = atomicAdd(&tpos[t], 1);
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
+  }
+}
+
+// Light-row tier t (light_tier_slots): its table size and workgroup width
+// fixed at compile time. light_tier_call(t, stream, n, &params, ..) launches
+// n rows; with params == nullptr it sets the kernel's LDS attribute instead.
+__host__ __device__ constexpr int light_tier_nt(int t) { return t == 0 ? 1024 : t == 3 ? 256 : 512; }
+inline int light_tier(int slots) {
+  int t = 0;
+  while (t + 1 < kLightTiers && light_tier_slots(t + 1) >= slots) ++t;
+  return t;
+}
+template <int T>
+int light_tier_go(hipStream_t st, int n, const CoocParams* lp) {
+  constexpr int NT = light_tier_nt(T), S = light_tier_slots(T);
+  const int lds = cooc_light_lds<NT, S>();
+  if (!lp) {
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<NT, S>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    return MR_OK;
+  }
+  hipLaunchKernelGGL((k_cooc_light<NT, S>), dim3(n), dim3(NT), (size_t)lds, st, *lp);
+  MR_HIP(hipGetLastError());
+  return MR_OK;
+}
+int light_tier_call(int t, hipStream_t st, int n, const CoocParams* lp, const CoocParams&) {
+  switch (t) {
+    case 0: return light_tier_go<0>(st, n, lp);
+    case 1: return light_tier_go<1>(st, n, lp);
+    case 2: return light_tier_go<2>(st, n, lp);
+    default: return light_tier_go<3>(st, n, lp);
   }
 }
 
@@ -2532,8 +2560,7 @@ struct mr_ctx {
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
-  int n_light_small = 0;           // the last light rows: <= kLightSmallSlots hash slots
-  int n_light_mid = 0;             // before them: <= kLightMidSlots
+  int n_light_tier[4] = {0, 0, 0, 0};  // light rows per table tier (light_tier_slots), in launch order
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
@@ -2556,7 +2583,8 @@ struct mr_ctx {
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     row_users.clear(); build_reads = 0;
-    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = n_light_small = n_light_mid = 0;
+    ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
+    for (int& x : n_light_tier) x = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
     if (graph) (void)hipGraphDestroy(graph);
     graph_exec = nullptr;
@@ -3289,8 +3317,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
     // heavy rows, then light rows with large tables, then the small-table ones
-    std::stable_partition(light_rows.begin(), light_rows.end(), [&](int32_t r) { return row_slots[r] > kLightSmallSlots; });
-    std::stable_partition(light_rows.begin(), light_rows.end(), [&](int32_t r) { return row_slots[r] > kLightMidSlots; });
+    std::stable_sort(light_rows.begin(), light_rows.end(), [&](int32_t x, int32_t y) {
+      return light_tier(row_slots[x]) < light_tier(row_slots[y]);
+    });
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
@@ -3379,18 +3408,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
-    c->n_light_small = c->n_light_mid = 0;
-    for (int32_t r : light_rows) {
-      c->n_light_small += row_slots[r] <= kLightSmallSlots ? 1 : 0;
-      c->n_light_mid += (row_slots[r] > kLightSmallSlots && row_slots[r] <= kLightMidSlots) ? 1 : 0;
-    }
-    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightNT, kLightSlots>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, cooc_light_lds<kLightNT, kLightSlots>()));
-    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightMidNT, kLightMidSlots>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, cooc_light_lds<kLightMidNT, kLightMidSlots>()));
-    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<kLightSmallNT, kLightSmallSlots>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                               cooc_light_lds<kLightSmallNT, kLightSmallSlots>()));
+    for (int& x : c->n_light_tier) x = 0;
+    for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r])]++;
+    for (int t = 0; t < kLightTiers; ++t)
+      if (int rc2 = light_tier_call(t, nullptr, 0, nullptr, CoocParams{})) return rc2;
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3571,29 +3592,13 @@ int run_cooc(mr_ctx* c) {
                          (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }
-    const int nl_big = c->n_light - c->n_light_small - c->n_light_mid;
-    if (nl_big > 0) {
+    int lr = c->n_heavy;
+    for (int t = 0; t < kLightTiers; ++t) {
+      if (c->n_light_tier[t] == 0) continue;
       CoocParams lp = cp;
-      lp.rows = c->rows_order.p + c->n_heavy;
-      const size_t lds = (size_t)cooc_light_lds<kLightNT, kLightSlots>();
-      hipLaunchKernelGGL((k_cooc_light<kLightNT, kLightSlots>), dim3(nl_big), dim3(kLightNT), lds, st, lp);
-      MR_HIP(hipGetLastError());
-    }
-    if (c->n_light_mid > 0) {
-      CoocParams lp = cp;
-      lp.rows = c->rows_order.p + c->n_heavy + nl_big;
-      const size_t lds = (size_t)cooc_light_lds<kLightMidNT, kLightMidSlots>();
-      hipLaunchKernelGGL((k_cooc_light<kLightMidNT, kLightMidSlots>), dim3(c->n_light_mid), dim3(kLightMidNT),
-                         lds, st, lp);
-      MR_HIP(hipGetLastError());
-    }
-    if (c->n_light_small > 0) {
-      CoocParams lp = cp;
-      lp.rows = c->rows_order.p + c->n_heavy + nl_big + c->n_light_mid;
-      const size_t lds = (size_t)cooc_light_lds<kLightSmallNT, kLightSmallSlots>();
-      hipLaunchKernelGGL((k_cooc_light<kLightSmallNT, kLightSmallSlots>), dim3(c->n_light_small), dim3(kLightSmallNT),
-                         lds, st, lp);
-      MR_HIP(hipGetLastError());
+      lp.rows = c->rows_order.p + lr;
+      if (int rc2 = light_tier_call(t, st, c->n_light_tier[t], &lp, lp)) return rc2;
+      lr += c->n_light_tier[t];
     }
   }
   if (timed) MR_HIP(hipEventRecord(ev[1], st));
