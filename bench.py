@@ -273,20 +273,27 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         songs, _sc, _k = ens.topk(models["lcm"])  # this rank's cell when world > 1
         ab = algorithmic_bytes(full, 4, 10)
         model_bytes = sum(ab.values())
+        ibm_bytes = model_bytes
+        if eng.ibm_route == "cooc":  # the ibm model's byte model on its route (an untimed run for the counts)
+            eng.run("ibm")
+            eng.sync()
+            ibm_bytes = sum(cooc_bytes(eng, ds, 4, 10).values())
         dense_elems = full.n_test * full.n_songs
         # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)
-        step_bytes = 2 * model_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
+        step_bytes = model_bytes + ibm_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
         step_s = elapsed / args.steps
         traffic = None
         pmc_file = os.path.join(ROOT, "profiles", "pmc_c5.json")
         if world == 1 and os.path.exists(pmc_file):  # per-step PMC sum (scripts/pmc_traffic.py step mode)
             with open(pmc_file) as f:
-                traffic = json.load(f).get("traffic_bytes_per_launch")
+                pmc = json.load(f)
+            if (pmc.get("ibm_route") or "two_hop") == eng.ibm_route:  # counters of the same ibm route only
+                traffic = pmc.get("traffic_bytes_per_launch")
         line = {
             "metric": "scored (test-user,song) pairs/sec, ensemble ubm+ibm+lcm+am+scm + threshold mAP",
             "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "int64",
+            "vs_baseline": None, "dtype": "int64", "ibm_route": eng.ibm_route,
             "data": "synthetic (bulk Zipf/lognormal Taste-Profile-shaped triplets, capped head, SURVEY.md §8d)",
             "config": {"workload": f"c5: {n_tr} train / {n_te} test / {full.n_songs} songs; ubm + ibm dense fp32, "
                                    f"linear(0.5) + aggregation(0.5) + stochastic(0.5, seed 1), threshold mAP x5",
