@@ -274,9 +274,7 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         ab = algorithmic_bytes(full, 4, 10)
         model_bytes = sum(ab.values())
         ibm_bytes = model_bytes
-        if eng.ibm_route == "cooc":  # the ibm model's byte model on its route (an untimed run for the counts)
-            eng.run("ibm")
-            eng.sync()
+        if eng.ibm_route == "cooc":  # the ibm model's byte model on its route (counts of the last ibm run)
             ibm_bytes = sum(cooc_bytes(eng, ds, 4, 10).values())
         dense_elems = full.n_test * full.n_songs
         # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)

@@ -168,12 +168,13 @@ int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_
  * (a bound on the shard's non-zero counts; 4 B each). Any pointer may be NULL. */
 int mr_route_info(const mr_ctx* ctx, int32_t* route, int32_t* n_rows, int64_t* pool_entries);
 
-/* Sizes of the last ibm run on the co-listening route (the byte model of
+/* Sizes of the latest ibm run on the co-listening route (the byte model of
  * bench.py's roofline; synchronous): *index_nnz = non-zero counts C[s2][s]
  * over all index rows and the shard's songs, *consumed = Σ_u Σ_{s2 ∈ T(u)}
  * (non-zeros of s2's row), *build_reads = Σ_rows (c_tr(s2) + Σ_{v ∈ L_tr(s2)}
  * |S(v) ∩ shard|) (the listener lists and their songs the build reads).
- * MR_E_STATE unless the context is on route 2 and ran ibm last. */
+ * MR_E_STATE unless the context is on route 2 and has run ibm since its load
+ * (the counts are those of the latest ibm run). */
 int mr_cooc_stats(mr_ctx* ctx, int64_t* index_nnz, int64_t* consumed, int64_t* build_reads);
 
 /* Host only, before any load: the song tile of the wide shape that a context

@@ -2559,6 +2559,7 @@ struct mr_ctx {
   DevBuf<unsigned> row_nnz;        // per run: each index row's non-zeros over the shard
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
+  bool cooc_ran = false;           // an ibm run on route 2 since the load (its row_nnz are current)
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
   int n_light_tier[4] = {0, 0, 0, 0};  // light rows per table tier (light_tier_slots), in launch order
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
@@ -2582,7 +2583,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    row_users.clear(); build_reads = 0;
+    row_users.clear(); build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
     for (int& x : n_light_tier) x = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
@@ -3457,7 +3458,7 @@ int mr_route_info(const mr_ctx* c, int32_t* route, int32_t* n_rows, int64_t* poo
 int mr_cooc_stats(mr_ctx* c, int64_t* index_nnz, int64_t* consumed, int64_t* build_reads) {
   if (!c) return fail(MR_E_INVALID, "null context");
   if (!c->loaded || c->ibm_route != 2) return fail(MR_E_STATE, "mr_cooc_stats needs a context on ibm_route 2");
-  if (!c->ran || c->last_model != MR_IBM) return fail(MR_E_STATE, "mr_cooc_stats before an ibm run");
+  if (!c->cooc_ran) return fail(MR_E_STATE, "mr_cooc_stats before an ibm run");
   MR_HIP(hipSetDevice(c->opt.device));
   std::vector<unsigned> nnz((size_t)std::max(1, c->n_rows), 0u);
   if (c->n_rows > 0)
@@ -3639,7 +3640,10 @@ int run_cooc(mr_ctx* c) {
 }
 
 int run_model(mr_ctx* c, int model) {
-  if (model == MR_IBM && c->ibm_route == 2) return run_cooc(c);
+  if (model == MR_IBM && c->ibm_route == 2) {
+    c->cooc_ran = true;
+    return run_cooc(c);
+  }
   hipStream_t st = c->stream;
   const bool timed = c->opt.time_kernels != 0;
   const int k = c->opt.topk;

@@ -108,7 +108,7 @@ class Engine:
 
     def cooc_stats(self) -> Tuple[int, int, int]:
         """(index non-zeros, entries consumed by the scoring, entries the build
-        reads) of the last ibm run on the co-listening route (mr_cooc_stats)."""
+        reads) of the latest ibm run on the co-listening route (mr_cooc_stats)."""
         a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         _lib.check(self._L.mr_cooc_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "mr_cooc_stats")
         return a.value, b.value, c.value

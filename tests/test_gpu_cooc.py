@@ -164,3 +164,29 @@ def test_route_errors():
     o.ibm_route = 3
     h = ctypes.c_void_p()
     assert _lib.lib().mr_create(ctypes.byref(o), ctypes.byref(h)) == _lib.MR_E_INVALID
+
+
+def test_cooc_stats_count_the_index(build_path):
+    """mr_cooc_stats: the index's non-zeros, the entries the scoring reads and
+    the build's reads, against a scipy count (bench.py's byte model uses them)."""
+    import scipy.sparse as sp
+
+    ds = synth.generate_bulk(20_000, 40, 3).dataset()
+    with Engine(ds, topk=10, dense=False, ibm_route="cooc") as e:
+        with pytest.raises(_lib.EngineError):
+            e.cooc_stats()  # no ibm run yet
+        e.run("ibm")
+        e.run("ubm")  # the counts stay those of the latest ibm run
+        index_nnz, consumed, reads = e.cooc_stats()
+    tr_rows = np.repeat(np.arange(ds.n_train), np.diff(ds.tr_off))
+    A = sp.csr_matrix((np.ones(tr_rows.size, np.int64), (tr_rows, ds.tr_songs)), shape=(ds.n_train, ds.n_songs))
+    c_tr = np.asarray(A.sum(axis=0)).ravel()
+    rows = np.unique(ds.te_songs)
+    rows = rows[c_tr[rows] > 0]
+    C = (A[:, rows].T @ A).tocsr()
+    nnz_r = np.diff(C.indptr)
+    users_r = np.bincount(np.searchsorted(rows, ds.te_songs[np.isin(ds.te_songs, rows)]), minlength=rows.size)
+    deg = np.diff(ds.tr_off)
+    assert index_nnz == int(nnz_r.sum())
+    assert consumed == int((nnz_r * users_r).sum())
+    assert reads == int(c_tr[rows].sum() + (A[:, rows].T @ deg).sum())
