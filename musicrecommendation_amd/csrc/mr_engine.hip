@@ -2560,6 +2560,8 @@ struct mr_ctx {
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   bool cooc_ran = false;           // an ibm run on route 2 since the load (its row_nnz are current)
+  hipStream_t side[2] = {nullptr, nullptr};  // light-row build streams (created with the context)
+  hipEvent_t side_fork = nullptr, side_join[2] = {nullptr, nullptr};
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
   int n_light_tier[4] = {0, 0, 0, 0};  // light rows per table tier (light_tier_slots), in launch order
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
@@ -2673,6 +2675,12 @@ int merge_rows_opt() {
 // (MR_COOC_LIGHT=0: A/B experiments and tests; read at each mr_load).
 bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
+  return !(e && std::atoi(e) == 0);
+}
+// Light rows on side streams (default) or on the context stream
+// (MR_COOC_SIDE=0: A/B experiments; read at each run).
+bool cooc_side_opt() {
+  const char* e = std::getenv("MR_COOC_SIDE");
   return !(e && std::atoi(e) == 0);
 }
 // Dense-segment rule of k_cooc_build (MR_COOC_DENSE_DIV, default kCoocDenseDiv;
@@ -2914,6 +2922,13 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
     delete c;
     return fail(MR_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->side_join[i], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    mr_destroy(c);
+    return fail(MR_E_HIP, "side streams: %s", hipGetErrorString(e));
+  }
   for (auto& ev : c->win) {
     e = hipEventCreate(&ev);
     if (e != hipSuccess) {
@@ -2947,6 +2962,11 @@ int mr_destroy(mr_ctx* c) {
   }
   for (auto& ev : c->ring) if (ev) (void)hipEventDestroy(ev);
   for (auto& ev : c->win) if (ev) (void)hipEventDestroy(ev);
+  for (int i = 0; i < 2; ++i) {
+    if (c->side[i]) { (void)hipStreamSynchronize(c->side[i]); (void)hipStreamDestroy(c->side[i]); }
+    if (c->side_join[i]) (void)hipEventDestroy(c->side_join[i]);
+  }
+  if (c->side_fork) (void)hipEventDestroy(c->side_fork);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return MR_OK;
@@ -3567,6 +3587,11 @@ int run_cooc(mr_ctx* c) {
   }
   if (c->n_rows > 0) {
     MR_HIP(hipMemsetAsync(c->row_nnz.p, 0, (size_t)c->n_rows * sizeof(unsigned), st));
+    const bool side = c->side[0] && c->n_light > 0 && cooc_side_opt();
+    if (side) {
+      MR_HIP(hipEventRecord(c->side_fork, st));
+      for (int i = 0; i < 2; ++i) MR_HIP(hipStreamWaitEvent(c->side[i], c->side_fork, 0));
+    }
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
@@ -3593,14 +3618,23 @@ int run_cooc(mr_ctx* c) {
                          (size_t)cooc_build_lds<true>(c->block_songs), st, hp);
       MR_HIP(hipGetLastError());
     }
+    // light rows on two side streams (tiers 0-1 and 2-3), concurrent with
+    // the heavy rows on the context stream: the launches' tails overlap
+    // (8 x 1 shards: most rows are light, 4 short launches per step)
     int lr = c->n_heavy;
     for (int t = 0; t < kLightTiers; ++t) {
       if (c->n_light_tier[t] == 0) continue;
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + lr;
-      if (int rc2 = light_tier_call(t, st, c->n_light_tier[t], &lp, lp)) return rc2;
+      hipStream_t ls = side ? c->side[t / 2] : st;
+      if (int rc2 = light_tier_call(t, ls, c->n_light_tier[t], &lp, lp)) return rc2;
       lr += c->n_light_tier[t];
     }
+    if (side)
+      for (int i = 0; i < 2; ++i) {
+        MR_HIP(hipEventRecord(c->side_join[i], c->side[i]));
+        MR_HIP(hipStreamWaitEvent(st, c->side_join[i], 0));
+      }
   }
   if (timed) MR_HIP(hipEventRecord(ev[1], st));
   for (int y0 = 0; y0 < c->n_te; y0 += 65528) {

@@ -112,6 +112,10 @@ case ",$STEPS," in *,cfgroute,*)
 esac
 # per-rank device time of C4 layouts, one rank at a time on this GPU: LAYOUTS="1x1,2x1,4x1,8x1"
 case ",$STEPS," in *,layouts,*) run layouts 900 python -u scripts/layout_probe.py ibm ${LAYOUTS:-1x1,2x1,4x1,8x1,2x4} ;; esac
+case ",$STEPS," in *,proflayouts,*)
+  export TMPDIR=/tmp
+  run prof_layouts 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_layouts" -o p -- python3 "$ROOT/scripts/layout_probe.py" ibm ${LAYOUTS:-8x1} ;;
+esac
 case ",$STEPS," in *,profc4cooc,*)
   export TMPDIR=/tmp
   run prof_c4_cooc 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_cooc" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc ;;
