@@ -2039,7 +2039,9 @@ constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
 // rows are latency-bound, so smaller tables = more workgroups per CU):
 // 4096 slots / 256 threads (7 per CU), 8192 / 512 (4), 16384 / 512 (2),
 // 32768 / 1024 (1). Tier 0 is the largest (launched first).
-constexpr int kLightTiers = 4;
+constexpr int kLightTiers = 6;     // tiers 4, 5 (2048 / 1024 slots): one wave per row (k_cooc_light_wave)
+constexpr int kWaveRowsPerBlock = 4;
+constexpr int kWaveMaxTiles = 64;  // the wave tiers' per-row tile counters
 __host__ __device__ constexpr int light_tier_slots(int t) { return 32768 >> t; }
 // a table of S slots holds a row whose entry bound is at most S * 4/5 (the
 // bound counts every listener's songs; the distinct ones are far fewer)
@@ -2285,13 +2287,125 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   }
 }
 
+// The smallest light rows, one wave per row (kWaveRowsPerBlock rows per
+// workgroup, each wave with its own table, tile counters and listener
+// descriptors in LDS): the same walk, hash and emission as k_cooc_light with
+// wave scans instead of block scans and no workgroup barriers, so 28 rows per
+// CU are in flight instead of 7 (the rows are latency-bound).
+template <int SW>
+__host__ __device__ constexpr int cooc_wave_bytes() { return SW * 4 + 2 * kWaveMaxTiles * 4 + 64 * 8 + 68 * 4; }
+template <int SW>
+__global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(CoocParams p, int n_launch) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ri = blockIdx.x * kWaveRowsPerBlock + w;
+  if (ri >= n_launch) return;  // the whole wave (no workgroup barrier below)
+  unsigned char* base = smem_raw + (size_t)w * cooc_wave_bytes<SW>();
+  long long* m_a = reinterpret_cast<long long*>(base);
+  unsigned* tab = reinterpret_cast<unsigned*>(m_a + 64);
+  int* tcnt = reinterpret_cast<int*>(tab + SW);
+  int* tpos = tcnt + kWaveMaxTiles;
+  int* m_pre = tpos + kWaveMaxTiles;
+  const int r = p.rows[ri];
+  const int S = p.row_slots[r];
+  const unsigned mask = (unsigned)S - 1u;
+  const int sh = 32 - __builtin_ctz((unsigned)S);
+  for (int i = lane; i < S; i += 64) tab[i] = 0u;
+  for (int i = lane; i < p.n_tiles; i += 64) { tcnt[i] = 0; tpos[i] = 0; }
+  const int s2 = p.row_song[r];
+  const long long la = p.trs_off[s2];
+  const int n = (int)(p.trs_off[s2 + 1] - la);
+  const int* lst = p.trs_users + la;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    long long a = 0;
+    int len = 0;
+    if (c0 + lane < n) {
+      const int v = lst[c0 + lane];
+      a = p.sr_off[v];
+      len = (int)(p.sr_off[v + 1] - a);
+    }
+    const int inc = wave_incl_scan(len);
+    const int pre = inc - len;
+    const int total = __shfl(inc, 63, 64);
+    wave_lds_sync();  // the previous chunk's readers are done with the descriptors
+    m_a[lane] = a - pre;
+    m_pre[lane] = pre;
+    if (lane == 0) m_pre[min(64, n - c0)] = total;
+    wave_lds_sync();
+    constexpr int U = 4;
+    int cur = -1, ce = 0;
+    long long co = 0;
+    for (int e0 = lane; e0 < total; e0 += U * 64) {
+      unsigned key[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int e = e0 + j * 64;
+        key[j] = ~0u;
+        if (e < total) {
+          while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_a[cur]; }
+          key[j] = p.sr_songs[co + e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (key[j] == ~0u) continue;
+        const unsigned tag = (key[j] + 1u) << kLightCntBits;
+        unsigned h = (key[j] * 2654435761u) >> sh;
+        for (;;) {
+          unsigned x = tab[h];
+          if (x == 0u) {
+            x = atomicCAS(&tab[h], 0u, tag | 1u);
+            if (x == 0u) break;
+          }
+          if ((x & ~kLightCntMask) == tag) { atomicAdd(&tab[h], 1u); break; }
+          h = (h + 1u) & mask;
+        }
+      }
+    }
+  }
+  wave_lds_sync();
+  const int bs = p.block_songs;
+  for (int i = lane; i < S; i += 64) {
+    const unsigned x = tab[i];
+    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
+  }
+  wave_lds_sync();
+  {
+    int run = 0;
+    for (int t0 = 0; t0 < p.n_tiles; t0 += 64) {
+      const int t = t0 + lane;
+      const int c = t < p.n_tiles ? tcnt[t] : 0;
+      const int inc = wave_incl_scan(c);
+      if (t < p.n_tiles) {
+        tpos[t] = run + inc - c;
+        p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
+        p.seg_len[(size_t)t * p.n_rows + r] = c;
+      }
+      run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) p.row_nnz[r] = (unsigned)run;
+  }
+  wave_lds_sync();
+  unsigned* out = p.pool + p.row_base[r];
+  for (int i = lane; i < S; i += 64) {
+    const unsigned x = tab[i];
+    if (x) {
+      const int key = (int)((x >> kLightCntBits) - 1u);
+      const int t = key / bs;
+      const int pos = atomicAdd(&tpos[t], 1);
+      out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
+    }
+  }
+}
+
 // Light-row tier t (light_tier_slots): its table size and workgroup width
 // fixed at compile time. light_tier_call(t, stream, n, &params, ..) launches
 // n rows; with params == nullptr it sets the kernel's LDS attribute instead.
 __host__ __device__ constexpr int light_tier_nt(int t) { return t == 0 ? 1024 : t == 3 ? 256 : 512; }
-inline int light_tier(int slots) {
+inline int light_tier(int slots, int n_tiles) {
+  const int last = n_tiles <= kWaveMaxTiles ? kLightTiers - 1 : 3;  // wave tiers hold <= 64 tile counters
   int t = 0;
-  while (t + 1 < kLightTiers && light_tier_slots(t + 1) >= slots) ++t;
+  while (t + 1 <= last && light_tier_slots(t + 1) >= slots) ++t;
   return t;
 }
 template <int T>
@@ -2306,12 +2420,26 @@ int light_tier_go(hipStream_t st, int n, const CoocParams* lp) {
   MR_HIP(hipGetLastError());
   return MR_OK;
 }
+template <int SW>
+int light_wave_go(hipStream_t st, int n, const CoocParams* lp) {
+  const int lds = cooc_wave_bytes<SW>() * kWaveRowsPerBlock;
+  if (!lp) {
+    MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light_wave<SW>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    return MR_OK;
+  }
+  hipLaunchKernelGGL(k_cooc_light_wave<SW>, dim3((n + kWaveRowsPerBlock - 1) / kWaveRowsPerBlock),
+                     dim3(64 * kWaveRowsPerBlock), (size_t)lds, st, *lp, n);
+  MR_HIP(hipGetLastError());
+  return MR_OK;
+}
 int light_tier_call(int t, hipStream_t st, int n, const CoocParams* lp, const CoocParams&) {
   switch (t) {
     case 0: return light_tier_go<0>(st, n, lp);
     case 1: return light_tier_go<1>(st, n, lp);
     case 2: return light_tier_go<2>(st, n, lp);
-    default: return light_tier_go<3>(st, n, lp);
+    case 3: return light_tier_go<3>(st, n, lp);
+    case 4: return light_wave_go<2048>(st, n, lp);
+    default: return light_wave_go<1024>(st, n, lp);
   }
 }
 
@@ -2563,7 +2691,7 @@ struct mr_ctx {
   hipStream_t side[2] = {nullptr, nullptr};  // light-row build streams (created with the context)
   hipEvent_t side_fork = nullptr, side_join[2] = {nullptr, nullptr};
   int n_heavy = 0, n_light = 0;    // rows built per (row, tile) / per row (k_cooc_light)
-  int n_light_tier[4] = {0, 0, 0, 0};  // light rows per table tier (light_tier_slots), in launch order
+  int n_light_tier[6] = {0, 0, 0, 0, 0, 0};  // light rows per table tier (light_tier_slots), in launch order
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
@@ -3339,7 +3467,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
     // heavy rows, then light rows with large tables, then the small-table ones
     std::stable_sort(light_rows.begin(), light_rows.end(), [&](int32_t x, int32_t y) {
-      return light_tier(row_slots[x]) < light_tier(row_slots[y]);
+      return light_tier(row_slots[x], n_tiles) < light_tier(row_slots[y], n_tiles);
     });
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
@@ -3430,7 +3558,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->force32 = cooc_dense32_opt();
     c->n_light = (int)light_rows.size();
     for (int& x : c->n_light_tier) x = 0;
-    for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r])]++;
+    for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r], n_tiles)]++;
     for (int t = 0; t < kLightTiers; ++t)
       if (int rc2 = light_tier_call(t, nullptr, 0, nullptr, CoocParams{})) return rc2;
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3626,7 +3754,7 @@ int run_cooc(mr_ctx* c) {
       if (c->n_light_tier[t] == 0) continue;
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + lr;
-      hipStream_t ls = side ? c->side[t / 2] : st;
+      hipStream_t ls = side ? c->side[t < 2 ? 0 : 1] : st;
       if (int rc2 = light_tier_call(t, ls, c->n_light_tier[t], &lp, lp)) return rc2;
       lr += c->n_light_tier[t];
     }
