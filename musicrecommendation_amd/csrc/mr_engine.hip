@@ -20,9 +20,16 @@
 //            rebuilds u's neighbour weights in LDS (k_score<.., FUSED=true>);
 //   separate (large train sets): k_neighbours writes compacted neighbour
 //            lists, then k_score<.., FUSED=false> reads them.
-// Integer accumulation is associative, so every launch geometry, shard count
-// and the CPU fixed-point oracle (oracle/fixedpoint.c) give bit-identical
-// scores and hence identical top-k order. Built with -ffp-contract=off.
+// ItemBasedModel on large train sets, the co-listening route (round 3,
+// DESIGN.md §4b): per run, an index of C[s2][s] = |L_tr(s2) ∩ L_tr(s)| for
+// every test-visible song s2 (k_cooc_light / k_cooc_light_wave: LDS hash per
+// row; k_cooc_build: LDS counters per (row, tile)), then per (u, tile)
+//       acc[s] = Σ_{s2 ∈ T(u)} q(s2) · C[s2][s]      (k_score_wide<.., COOC>)
+//   — the same int64 sum as stage 1 + stage 2 with the two sums exchanged.
+// Integer accumulation is associative, so every launch geometry, shard count,
+// route and the CPU fixed-point oracle (oracle/fixedpoint.c) give
+// bit-identical scores and hence identical top-k order. Built with
+// -ffp-contract=off.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1542,6 +1549,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
+#ifndef MR_WIDE_EB
+#define MR_WIDE_EB 8        // wide-kernel epilogue: songs per thread whose scale loads are issued together
+#endif
 #ifndef MR_COOC_U
 #define MR_COOC_U 4         // co-listening route: 16-B pool loads (4 entries) per thread in flight
 #endif
@@ -1896,7 +1906,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
   long long mk = kKeyNone;
   int ms = INT_MAX;
-  constexpr int EB = 8;
+  constexpr int EB = MR_WIDE_EB;
   for (int i0 = tid; i0 < bw; i0 += EB * NT) {
     double sc[EB];
     unsigned long long av[EB];
