@@ -1576,8 +1576,13 @@ typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // tiles <= 32768 songs and counts < 131072 (mr_load checks both).
 constexpr int kCoocCntBits = 17;
 // seg_len of a dense segment (counts of every song of the tile, u16 / u32)
+// seg_len of a dense segment: -1 = u16 counts of every song of the tile;
+// <= -3 = u16 counts saturated at the build's sat value (rows with >= 65536
+// listeners), followed by -seg_len - 3 sparse entries carrying each larger
+// count's excess (count - sat) — the dense pass adds min(count, sat) · q, the
+// sparse walk the rest
 constexpr int kCoocDense16 = -1;
-constexpr int kCoocDense32 = -2;
+constexpr int kCoocDenseTail = -3;
 constexpr int kCoocDenseDiv = 3;
 constexpr int kCoocBigRow = 4096;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
@@ -1755,7 +1760,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     for (long long c0 = t0; c0 < t1; c0 += p.nseg) {
       const int ns = (int)min<long long>(p.nseg, t1 - c0);
       int len = 0, isd = 0, fmt = 0;
-      long long off = 0;
+      long long off = 0, tail_off = -1;
       unsigned long long q = 0ull;
       if (tid < ns) {
         const int r = p.te_row[c0 + tid];
@@ -1763,14 +1768,23 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           const int sl = slen[r];
           off = soff[r];
           q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
-          if (sl < 0) { isd = 1; fmt = sl; } else { len = sl; }
+          if (sl < 0) {
+            isd = 1;
+            fmt = kCoocDense16;
+            if (sl <= kCoocDenseTail) {  // saturated u16 words, then the excess entries
+              len = kCoocDenseTail - sl;
+              tail_off = off + (((bw + 1) / 2 + 3) & ~3);
+            }
+          } else {
+            len = sl;
+          }
         }
       }
       int total, nd;
       const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
       const int dpre = block_excl_scan_nt<NT>(isd, &nd, s_scan);
       if (tid < ns) {
-        m_off[tid] = off - pre;
+        m_off[tid] = (tail_off >= 0 ? tail_off : off) - pre;
         m_q[tid] = q;
         m_pre[tid] = pre;
         if (isd) { d_off[dpre] = off; d_q[dpre] = q; d_fmt[dpre] = fmt; }
@@ -1786,37 +1800,23 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           // DU dense rows per step, their loads issued together
           constexpr int DU = MR_COOC_DU;
           for (int d0 = 0; d0 < nd; d0 += DU) {
-            uint4 v0[DU], v1[DU];
+            uint4 v0[DU];
             unsigned long long qd[DU];
-            bool w16[DU];
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               const int d = d0 + j;
               qd[j] = 0ull;
-              w16[j] = true;
-              v0[j] = v1[j] = make_uint4(0u, 0u, 0u, 0u);
+              v0[j] = make_uint4(0u, 0u, 0u, 0u);
               if (d < nd) {
-                const unsigned* seg = p.pool + d_off[d];
                 qd[j] = d_q[d];
-                w16[j] = d_fmt[d] == kCoocDense16;
-                if (w16[j]) {
-                  v0[j] = *reinterpret_cast<const uint4*>(seg + (b0 >> 1));
-                } else {
-                  v0[j] = *reinterpret_cast<const uint4*>(seg + b0);
-                  v1[j] = *reinterpret_cast<const uint4*>(seg + b0 + 4);
-                }
+                v0[j] = *reinterpret_cast<const uint4*>(p.pool + d_off[d] + (b0 >> 1));
               }
             }
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               unsigned c8[8];
-              if (w16[j]) {
-                c8[0] = v0[j].x & 0xffffu; c8[1] = v0[j].x >> 16; c8[2] = v0[j].y & 0xffffu; c8[3] = v0[j].y >> 16;
-                c8[4] = v0[j].z & 0xffffu; c8[5] = v0[j].z >> 16; c8[6] = v0[j].w & 0xffffu; c8[7] = v0[j].w >> 16;
-              } else {
-                c8[0] = v0[j].x; c8[1] = v0[j].y; c8[2] = v0[j].z; c8[3] = v0[j].w;
-                c8[4] = v1[j].x; c8[5] = v1[j].y; c8[6] = v1[j].z; c8[7] = v1[j].w;
-              }
+              c8[0] = v0[j].x & 0xffffu; c8[1] = v0[j].x >> 16; c8[2] = v0[j].y & 0xffffu; c8[3] = v0[j].y >> 16;
+              c8[4] = v0[j].z & 0xffffu; c8[5] = v0[j].z >> 16; c8[6] = v0[j].w & 0xffffu; c8[7] = v0[j].w >> 16;
 #pragma unroll
               for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd[j];
             }
@@ -2016,7 +2016,8 @@ struct CoocParams {
   const unsigned* sr_songs;
   const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
   int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
-  int force32;                   // 1: dense counts as u32 even below 65536 listeners (tests)
+  int force32;                   // 1: every heavy row as a >= 65536-listener row (tests: the saturated format)
+  unsigned sat;                  // saturation of those rows' u16 dense counts (65535; tests lower it)
   long long* stamps;             // diagnostic build: [workgroup][8] s_memrealtime at phase ends
   unsigned* row_nnz;             // [n_rows] non-zero counts of the row over the shard (zeroed per run)
   int n_big;                     // k_cooc_build: the first n_big rows of the launch one workgroup per
@@ -2092,7 +2093,7 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
   const long long a = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - a);
   const int* lst = p.trs_users + a;
-  const bool c16 = n < 65536 && !p.force32;
+  const bool c16 = n < 65536 && !p.force32;  // else: saturated u16 + excess tail
   constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
   auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
 #pragma unroll
@@ -2134,11 +2135,8 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
     // it) or u32, no index and no atomics on the consumer side. Segments are
     // whole 16-B words (32-B for u32 counts: read 8 songs at a time).
     const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
-    const int words = dense ? (c16 ? ((bw + 1) / 2 + 3) & ~3 : (bw + 7) & ~7) : (total + 3) & ~3;
-    if (tid == 0) {
-      p.seg_off[(size_t)tile * p.n_rows + r] = off;
-      p.seg_len[(size_t)tile * p.n_rows + r] = dense ? (c16 ? kCoocDense16 : kCoocDense32) : total;
-    }
+    const int dwords = ((bw + 1) / 2 + 3) & ~3;  // a dense segment's u16 words, whole 16-B words
+    int words = dense ? dwords : (total + 3) & ~3;
     unsigned* out = p.pool + off;
     if (dense) {
       if (c16) {
@@ -2146,15 +2144,43 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
           if constexpr (P16) out[i] = cnt[i];  // the LDS words are the u16 pairs already
           else out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
         }
+        if (tid == 0) {
+          p.seg_off[(size_t)tile * p.n_rows + r] = off;
+          p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDense16;
+        }
       } else {
-        for (int i = tid; i < bw; i += NT) out[i] = count_of(i);
+        // counts above sat (only songs heard by >= sat users): saturated in
+        // the u16 words, their excess as sparse entries after them
+        if (tid == 0) *s_nz = 0;
+        __syncthreads();
+        for (int i = tid; 2 * i < bw; i += NT) {
+          const unsigned c0 = count_of(2 * i), c1 = 2 * i + 1 < bw ? count_of(2 * i + 1) : 0u;
+          out[i] = min(c0, p.sat) | (min(c1, p.sat) << 16);
+          if (c0 > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)(2 * i) << kCoocCntBits) | (c0 - p.sat);
+          if (c1 > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)(2 * i + 1) << kCoocCntBits) | (c1 - p.sat);
+        }
+        __syncthreads();
+        const int tail = *s_nz;
+        words = (dwords + tail + 3) & ~3;
+        if (tid == 0) {
+          p.seg_off[(size_t)tile * p.n_rows + r] = off;
+          p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDenseTail - tail;
+        }
       }
     } else if (total <= kCap) {  // the touched list holds every non-zero song
+      if (tid == 0) {
+        p.seg_off[(size_t)tile * p.n_rows + r] = off;
+        p.seg_len[(size_t)tile * p.n_rows + r] = total;
+      }
       for (int k = tid; k < total; k += NT) {
         const unsigned x = touched[k];
         out[k] = (x << kCoocCntBits) | count_of((int)x);
       }
     } else {  // song-ordered compaction: wave w owns songs [wb, we), offsets by ballots
+      if (tid == 0) {
+        p.seg_off[(size_t)tile * p.n_rows + r] = off;
+        p.seg_len[(size_t)tile * p.n_rows + r] = total;
+      }
       const int q4 = (bw + NT - 1) / NT * 64;
       const int wb = min(bw, w * q4), we = min(bw, wb + q4);
       int nz = 0;
@@ -2705,6 +2731,7 @@ struct mr_ctx {
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
+  unsigned sat = 65535;
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
   DevBuf<long long> sr_off;        // light rows: the shard's train rows
@@ -2831,6 +2858,13 @@ int cooc_dense_div_opt() {
 int cooc_dense32_opt() {
   const char* e = std::getenv("MR_COOC_DENSE32");
   return e && std::atoi(e) == 1 ? 1 : 0;
+}
+// Saturation of the u32-counter rows' u16 dense counts (65535; MR_COOC_SAT
+// lowers it so tests see excess entries on small data).
+unsigned cooc_sat_opt() {
+  const char* e = std::getenv("MR_COOC_SAT");
+  const long v = e ? std::atol(e) : 65535;
+  return (unsigned)std::min<long>(65535, std::max<long>(1, v));
 }
 
 // Auto route rule: the co-listening route when its estimated device time is
@@ -3387,17 +3421,19 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       }
       // heavy rows whose counts may pass 65535 first (u32 counters), the rest
       // keep their order (u16-pair counters, k_cooc_build<.., true>)
+      const bool all32 = !MR_COOC_P16 || cooc_dense32_opt();
       std::stable_partition(heavy_rows.begin(), heavy_rows.end(), [&](int32_t r) {
-        return !MR_COOC_P16 || col_tr[row_song[r]] >= 65536;
+        return all32 || col_tr[row_song[r]] >= 65536;
       });
-      for (int32_t r : heavy_rows) n_heavy32 += (!MR_COOC_P16 || col_tr[row_song[r]] >= 65536) ? 1 : 0;
+      for (int32_t r : heavy_rows) n_heavy32 += (all32 || col_tr[row_song[r]] >= 65536) ? 1 : 0;
       // Big rows (>= kCoocBigRow listeners, and every u32 row): one workgroup
       // per (row, tile), each tile a fixed slot of tcap words (the larger of a
       // dense segment and the longest sparse one), so the row's tiles run in
       // parallel. Rows are heaviest first, so the big rows of each kind lead.
       const int sparse_max = dense_div > 0 ? (bs + dense_div - 1) / dense_div : bs;
-      tcap32 = (std::max(sparse_max, bs) + 7) & ~7;
-      tcap16 = cooc_dense32_opt() ? tcap32 : (std::max(sparse_max, (bs + 1) / 2) + 7) & ~7;
+      // u32-counter rows: saturated u16 words + at most one excess entry per song
+      tcap32 = (std::max(sparse_max, (((bs + 1) / 2 + 3) & ~3) + bs) + 7) & ~7;
+      tcap16 = (std::max(sparse_max, (bs + 1) / 2) + 7) & ~7;
       n_big16 = 0;
       for (size_t i = n_heavy32; i < heavy_rows.size(); ++i) {
         if (col_tr[row_song[heavy_rows[i]]] < kCoocBigRow) break;
@@ -3566,6 +3602,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->tcap32 = tcap32;
     c->dense_div = dense_div;
     c->force32 = cooc_dense32_opt();
+    c->sat = cooc_sat_opt();
     c->n_light = (int)light_rows.size();
     for (int& x : c->n_light_tier) x = 0;
     for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r], n_tiles)]++;
@@ -3733,8 +3770,9 @@ int run_cooc(mr_ctx* c) {
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
-                  c->dense_div, c->force32, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
+                  c->dense_div, c->force32, 65535u, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
                   c->row_nnz.p};
+    cp.sat = c->sat;
     // heavy rows: >= 65536 listeners with u32 counters, then the rest with u16 pairs
     const int n32 = c->n_heavy32, n16 = c->n_heavy - c->n_heavy32;
     if (n32 > 0) {  // all big: one workgroup per (row, tile)

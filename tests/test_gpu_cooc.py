@@ -44,19 +44,26 @@ def check_route_exact(ds, *, k=10, **kw):
 # Index build paths (engine environment read at mr_load): light rows by the
 # LDS hash (default) or every row per (row, tile) (MR_COOC_LIGHT=0); tile
 # segments dense when a third of the songs are non-zero (default), always
-# (MR_COOC_DENSE_DIV=1000000, u16 or, with MR_COOC_DENSE32=1, u32 counts) or never (0).
+# (MR_COOC_DENSE_DIV=1000000) or never (0); MR_COOC_DENSE32=1 puts every heavy
+# row on the u32-counter kernel (saturated u16 words + excess entries, the
+# format of rows with >= 65536 listeners), MR_COOC_SAT lowers the saturation.
 BUILD_PATHS = {
     "light": {},
     "tiled": {"MR_COOC_LIGHT": "0"},
     "sparse": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "0"},
     "dense16": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000"},
     "dense32": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000", "MR_COOC_DENSE32": "1"},
+    # every heavy row on the u32-counter kernel, dense counts saturated at 2:
+    # the excess entries after the u16 words (the format of >= 65536-listener rows)
+    "dense_tail": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000", "MR_COOC_DENSE32": "1",
+                   "MR_COOC_SAT": "2"},
+    "mixed_tail": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE32": "1", "MR_COOC_SAT": "3"},
 }
 
 
 @pytest.fixture(params=list(BUILD_PATHS))
 def build_path(request, monkeypatch):
-    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32"):
+    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT"):
         monkeypatch.delenv(key, raising=False)
     for key, val in BUILD_PATHS[request.param].items():
         monkeypatch.setenv(key, val)
