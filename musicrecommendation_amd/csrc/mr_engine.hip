@@ -1576,13 +1576,12 @@ typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // tiles <= 32768 songs and counts < 131072 (mr_load checks both).
 constexpr int kCoocCntBits = 17;
 // seg_len of a dense segment (counts of every song of the tile, u16 / u32)
-// seg_len of a dense segment: -1 = u16 counts of every song of the tile;
-// <= -3 = u16 counts saturated at the build's sat value (rows with >= 65536
-// listeners), followed by -seg_len - 3 sparse entries carrying each larger
-// count's excess (count - sat) — the dense pass adds min(count, sat) · q, the
-// sparse walk the rest
-constexpr int kCoocDense16 = -1;
+// seg_len of a dense segment (<= -3): a byte per song of the tile, the count
+// saturated at the build's sat value (255), then -seg_len - 3 sparse entries
+// carrying each larger count's excess (count - sat) — the dense pass adds
+// min(count, sat) · q, the sparse walk the rest
 constexpr int kCoocDenseTail = -3;
+__host__ __device__ inline int cooc_dense_words(int bw) { return ((bw + 3) / 4 + 3) & ~3; }
 constexpr int kCoocDenseDiv = 3;
 constexpr int kCoocBigRow = 4096;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
@@ -1768,13 +1767,11 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           const int sl = slen[r];
           off = soff[r];
           q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
-          if (sl < 0) {
+          if (sl < 0) {  // saturated count bytes, then the excess entries
             isd = 1;
-            fmt = kCoocDense16;
-            if (sl <= kCoocDenseTail) {  // saturated u16 words, then the excess entries
-              len = kCoocDenseTail - sl;
-              tail_off = off + (((bw + 1) / 2 + 3) & ~3);
-            }
+            fmt = sl;
+            len = kCoocDenseTail - sl;
+            tail_off = off + cooc_dense_words(bw);
           } else {
             len = sl;
           }
@@ -1800,23 +1797,26 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           // DU dense rows per step, their loads issued together
           constexpr int DU = MR_COOC_DU;
           for (int d0 = 0; d0 < nd; d0 += DU) {
-            uint4 v0[DU];
+            uint2 v0[DU];
             unsigned long long qd[DU];
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               const int d = d0 + j;
               qd[j] = 0ull;
-              v0[j] = make_uint4(0u, 0u, 0u, 0u);
+              v0[j] = make_uint2(0u, 0u);
               if (d < nd) {
                 qd[j] = d_q[d];
-                v0[j] = *reinterpret_cast<const uint4*>(p.pool + d_off[d] + (b0 >> 1));
+                v0[j] = *reinterpret_cast<const uint2*>(p.pool + d_off[d] + (b0 >> 2));
               }
             }
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               unsigned c8[8];
-              c8[0] = v0[j].x & 0xffffu; c8[1] = v0[j].x >> 16; c8[2] = v0[j].y & 0xffffu; c8[3] = v0[j].y >> 16;
-              c8[4] = v0[j].z & 0xffffu; c8[5] = v0[j].z >> 16; c8[6] = v0[j].w & 0xffffu; c8[7] = v0[j].w >> 16;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                c8[i] = (v0[j].x >> (8 * i)) & 0xffu;
+                c8[4 + i] = (v0[j].y >> (8 * i)) & 0xffu;
+              }
 #pragma unroll
               for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd[j];
             }
@@ -2017,7 +2017,7 @@ struct CoocParams {
   const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
   int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
   int force32;                   // 1: every heavy row as a >= 65536-listener row (tests: the saturated format)
-  unsigned sat;                  // saturation of those rows' u16 dense counts (65535; tests lower it)
+  unsigned sat;                  // saturation of the dense count bytes (255; tests lower it)
   long long* stamps;             // diagnostic build: [workgroup][8] s_memrealtime at phase ends
   unsigned* row_nnz;             // [n_rows] non-zero counts of the row over the shard (zeroed per run)
   int n_big;                     // k_cooc_build: the first n_big rows of the launch one workgroup per
@@ -2093,7 +2093,6 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
   const long long a = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - a);
   const int* lst = p.trs_users + a;
-  const bool c16 = n < 65536 && !p.force32;  // else: saturated u16 + excess tail
   constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
   auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
 #pragma unroll
@@ -2131,41 +2130,35 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
     __syncthreads();
     const int total = *s_nz;
     // Dense segment when at least a third of the tile's songs are non-zero:
-    // every song's count as u16 (listener count < 65536: no count can exceed
-    // it) or u32, no index and no atomics on the consumer side. Segments are
-    // whole 16-B words (32-B for u32 counts: read 8 songs at a time).
+    // a count byte per song (no index, no atomics on the consumer side; the
+    // rare counts above sat carried by excess entries). Segments are whole
+    // 16-B words.
     const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
-    const int dwords = ((bw + 1) / 2 + 3) & ~3;  // a dense segment's u16 words, whole 16-B words
-    int words = dense ? dwords : (total + 3) & ~3;
+    const int dwords = cooc_dense_words(bw);  // a dense segment's u8 count words, whole 16-B words
+    int words = (total + 3) & ~3;
     unsigned* out = p.pool + off;
     if (dense) {
-      if (c16) {
-        for (int i = tid; 2 * i < bw; i += NT) {
-          if constexpr (P16) out[i] = cnt[i];  // the LDS words are the u16 pairs already
-          else out[i] = cnt[2 * i] | ((2 * i + 1 < bw ? cnt[2 * i + 1] : 0u) << 16);
+      // every song's count as a byte saturated at sat (255), the excess
+      // (count - sat) of the few larger counts as sparse entries after them
+      if (tid == 0) *s_nz = 0;
+      __syncthreads();
+      for (int i = tid; 4 * i < bw; i += NT) {
+        unsigned wv = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = 4 * i + j;
+          const unsigned c = col < bw ? count_of(col) : 0u;
+          wv |= min(c, p.sat) << (8 * j);
+          if (c > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
         }
-        if (tid == 0) {
-          p.seg_off[(size_t)tile * p.n_rows + r] = off;
-          p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDense16;
-        }
-      } else {
-        // counts above sat (only songs heard by >= sat users): saturated in
-        // the u16 words, their excess as sparse entries after them
-        if (tid == 0) *s_nz = 0;
-        __syncthreads();
-        for (int i = tid; 2 * i < bw; i += NT) {
-          const unsigned c0 = count_of(2 * i), c1 = 2 * i + 1 < bw ? count_of(2 * i + 1) : 0u;
-          out[i] = min(c0, p.sat) | (min(c1, p.sat) << 16);
-          if (c0 > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)(2 * i) << kCoocCntBits) | (c0 - p.sat);
-          if (c1 > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)(2 * i + 1) << kCoocCntBits) | (c1 - p.sat);
-        }
-        __syncthreads();
-        const int tail = *s_nz;
-        words = (dwords + tail + 3) & ~3;
-        if (tid == 0) {
-          p.seg_off[(size_t)tile * p.n_rows + r] = off;
-          p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDenseTail - tail;
-        }
+        out[i] = wv;
+      }
+      __syncthreads();
+      const int tail = *s_nz;
+      words = (dwords + tail + 3) & ~3;
+      if (tid == 0) {
+        p.seg_off[(size_t)tile * p.n_rows + r] = off;
+        p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDenseTail - tail;
       }
     } else if (total <= kCap) {  // the touched list holds every non-zero song
       if (tid == 0) {
@@ -2731,7 +2724,7 @@ struct mr_ctx {
   int n_heavy32 = 0;               // the first heavy rows: >= 65536 listeners (u32 counters)
   int n_big16 = 0, tcap16 = 0, tcap32 = 0;  // big u16 rows after them; per-tile slot words
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
-  unsigned sat = 65535;
+  unsigned sat = 255;
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
   DevBuf<long long> sr_off;        // light rows: the shard's train rows
@@ -2859,12 +2852,12 @@ int cooc_dense32_opt() {
   const char* e = std::getenv("MR_COOC_DENSE32");
   return e && std::atoi(e) == 1 ? 1 : 0;
 }
-// Saturation of the u32-counter rows' u16 dense counts (65535; MR_COOC_SAT
-// lowers it so tests see excess entries on small data).
+// Saturation of the dense segments' count bytes (255; MR_COOC_SAT lowers it
+// so tests see excess entries on small data).
 unsigned cooc_sat_opt() {
   const char* e = std::getenv("MR_COOC_SAT");
-  const long v = e ? std::atol(e) : 65535;
-  return (unsigned)std::min<long>(65535, std::max<long>(1, v));
+  const long v = e ? std::atol(e) : 255;
+  return (unsigned)std::min<long>(255, std::max<long>(1, v));
 }
 
 // Auto route rule: the co-listening route when its estimated device time is
@@ -3413,9 +3406,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           // k_cooc_build: a tile's segment is sparse (its non-zeros) or dense
           // (<= kCoocDenseDiv x its non-zeros, <= the tile's songs), in whole
           // 16-B words (32-B for u32 counts)
+          // (dense: count bytes <= kCoocDenseDiv / 4 x the non-zeros, + excess entries <= the non-zeros)
           const int64_t nz = row_base[r];
           const int64_t dn = std::max<int64_t>(1, std::min<int64_t>(dense_div, width)) * nz;
-          row_base[r] = ((std::min<int64_t>(width, dn) + 3) & ~(int64_t)3) + 8 * (int64_t)n_tiles;
+          row_base[r] = ((std::min<int64_t>(width, dn) + nz + 3) & ~(int64_t)3) + 8 * (int64_t)n_tiles;
           heavy_rows.push_back((int32_t)r);
         }
       }
@@ -3431,9 +3425,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // dense segment and the longest sparse one), so the row's tiles run in
       // parallel. Rows are heaviest first, so the big rows of each kind lead.
       const int sparse_max = dense_div > 0 ? (bs + dense_div - 1) / dense_div : bs;
-      // u32-counter rows: saturated u16 words + at most one excess entry per song
-      tcap32 = (std::max(sparse_max, (((bs + 1) / 2 + 3) & ~3) + bs) + 7) & ~7;
-      tcap16 = (std::max(sparse_max, (bs + 1) / 2) + 7) & ~7;
+      // a dense segment: the count bytes + at most one excess entry per song
+      tcap32 = (std::max(sparse_max, cooc_dense_words(bs) + bs) + 7) & ~7;
+      tcap16 = tcap32;
       n_big16 = 0;
       for (size_t i = n_heavy32; i < heavy_rows.size(); ++i) {
         if (col_tr[row_song[heavy_rows[i]]] < kCoocBigRow) break;
@@ -3770,7 +3764,7 @@ int run_cooc(mr_ctx* c) {
     CoocParams cp{c->n_tr, c->n_rows, c->n_tiles, c->block_songs, c->song_lo, c->song_hi, c->toff.p, c->tsongs.p,
                   c->trs_off.p, c->trs_users.p, c->row_song.p, c->row_base.p, c->pool.p,
                   c->seg_off.p, c->seg_len.p, c->rows_order.p, c->sr_off.p, c->sr_songs.p, c->row_slots.p,
-                  c->dense_div, c->force32, 65535u, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
+                  c->dense_div, c->force32, 255u, c->stamps.p ? c->stamps.p + c->bstamp_off : nullptr,
                   c->row_nnz.p};
     cp.sat = c->sat;
     // heavy rows: >= 65536 listeners with u32 counters, then the rest with u16 pairs
