@@ -2071,7 +2071,8 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
   const int bs = p.block_songs;
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
   int* s_scan = reinterpret_cast<int*>(smem_raw + align16(cooc_words<P16>(bs) * 4));
-  int* s_nz = s_scan + 16;
+  int* s_nz = s_scan + 16;      // songs first touched in this tile
+  int* s_tail = s_scan + 17;    // excess entries of this tile's dense segment
   unsigned short* touched = reinterpret_cast<unsigned short*>(s_scan + 16 + 8);
   constexpr int kCap = cooc_list_cap<P16>();
   auto count_of = [&](int i) -> unsigned {
@@ -2111,7 +2112,7 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
     const int blo = p.song_lo + tile * bs;
     const int bw = min(p.song_hi, blo + bs) - blo;
     for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
-    if (tid == 0) *s_nz = 0;
+    if (tid == 0) { *s_nz = 0; *s_tail = 0; }
     __syncthreads();
     walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
                                            [&](unsigned x, unsigned) {
@@ -2140,8 +2141,7 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
     if (dense) {
       // every song's count as a byte saturated at sat (255), the excess
       // (count - sat) of the few larger counts as sparse entries after them
-      if (tid == 0) *s_nz = 0;
-      __syncthreads();
+      // (own counter: s_nz is still being read for `total` by other waves)
       for (int i = tid; 4 * i < bw; i += NT) {
         unsigned wv = 0u;
 #pragma unroll
@@ -2149,12 +2149,12 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
           const int col = 4 * i + j;
           const unsigned c = col < bw ? count_of(col) : 0u;
           wv |= min(c, p.sat) << (8 * j);
-          if (c > p.sat) out[dwords + atomicAdd(s_nz, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
+          if (c > p.sat) out[dwords + atomicAdd(s_tail, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
         }
         out[i] = wv;
       }
       __syncthreads();
-      const int tail = *s_nz;
+      const int tail = *s_tail;
       words = (dwords + tail + 3) & ~3;
       if (tid == 0) {
         p.seg_off[(size_t)tile * p.n_rows + r] = off;
