@@ -1583,7 +1583,10 @@ constexpr int kCoocCntBits = 17;
 constexpr int kCoocDenseTail = -3;
 __host__ __device__ inline int cooc_dense_words(int bw) { return ((bw + 3) / 4 + 3) & ~3; }
 constexpr int kCoocDenseDiv = 3;
-constexpr int kCoocBigRow = 4096;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
+#ifndef MR_COOC_BIG_ROW
+#define MR_COOC_BIG_ROW 4096
+#endif
+constexpr int kCoocBigRow = MR_COOC_BIG_ROW;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
 constexpr int kCoocMaxTile = 1 << (32 - kCoocCntBits);
 
