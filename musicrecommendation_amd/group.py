@@ -39,7 +39,8 @@ def song_shards_native(ds: Dataset, n_shards: int, tile: int = 0) -> List[Tuple[
 class Group:
     def __init__(self, dataset: Dataset, *, song_shards: int = 1, user_blocks: int = 1,
                  devices: Optional[Sequence[int]] = None, transport: str = "auto", frac_bits: int = 32,
-                 out_dtype: str = "f32", topk: int = 10, dense: bool = True, stage1: str = "auto"):
+                 out_dtype: str = "f32", topk: int = 10, dense: bool = True, stage1: str = "auto",
+                 ibm_route: str = "auto"):
         self._L = _lib.lib()
         opt = _lib.MrOptions()
         _lib.check(self._L.mr_options_default(ctypes.byref(opt)), "mr_options_default")
@@ -48,6 +49,7 @@ class Group:
         opt.topk = topk
         opt.dense = 1 if dense else 0
         opt.stage1 = _lib.STAGE1[stage1]
+        opt.ibm_route = {"auto": 0, "two_hop": 1, "cooc": 2}[ibm_route]  # mr_options.ibm_route
         go = _lib.MrGroupOptions()
         _lib.check(self._L.mr_group_options_default(ctypes.byref(go)), "mr_group_options_default")
         go.n_song_shards, go.n_user_blocks = song_shards, user_blocks

@@ -307,6 +307,33 @@ def test_multi_context_rccl_path_equals_one_context(layout, dense, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", [(2, 1), (3, 1), (2, 2)])
+@pytest.mark.parametrize("transport", ["copy", "rccl"])
+def test_group_colistening_route_equals_one_context(layout, transport, monkeypatch):
+    """The ItemBasedModel's co-listening route (mr_options.ibm_route = 2) in
+    every context of a group — each shard's index over its own songs, each
+    user block's over its own users' songs — merged lists and the dense model
+    bitwise equal to one two-hop context (copy transport, and the RCCL
+    transport through the fake RCCL on one GPU)."""
+    from musicrecommendation_amd.engine import Engine
+
+    if transport == "rccl":
+        monkeypatch.setenv("MR_RCCL_LIB", FAKE_RCCL)
+    gs, gu = layout
+    ds = synth.generate_bulk(20_000, 24, 6).dataset()
+    with Engine(ds, out_dtype="f64", topk=10, ibm_route="two_hop") as e:
+        e.run("ibm")
+        d_ref, (s_ref, _sc, k_ref) = e.dense(), e.topk()
+    with Group(ds, song_shards=gs, user_blocks=gu, transport=transport, out_dtype="f64", topk=10,
+               ibm_route="cooc") as g:
+        for _ in range(2):
+            g.run("ibm")
+            songs, _scores, keys = g.topk()
+            assert np.array_equal(songs, s_ref) and np.array_equal(keys, k_ref), (layout, transport)
+            assert np.array_equal(g.dense(), d_ref, equal_nan=True), (layout, transport)
+
+
+@pytest.mark.gpu
 def test_group_load_validates_before_sharding():
     """mr_group_load runs mr_load's checks before it reads the dataset itself
     (the shard balance indexes by song id): out-of-range ids, unsorted rows and
