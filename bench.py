@@ -14,14 +14,17 @@ scores test users [10r, 10r+10) of a 500 x 10N dataset over all songs, an
 exact partition of the model's pairs, no data-path collective — C2 is one
 ~12 us latency-bound launch, SURVEY.md §8e: "C2 is too small to scale"). The
 C2 line carries a nested ``north_star`` block at every N, including 1: C4
-(1M train / 10k test / 384,546 songs, top-10) in the north star's 2-D layout
-(sharding.ShardScorer: G_s song shards = 1 at N = 1, 2 at even N, x N/G_s
-test-user blocks; ONE RCCL all-gather of the packed top-k record blocks per
-step inside each block, merged on the device), strong scaling over the fixed
-test set: slowest-rank ms per step, exchange ms, all-gather bytes and the
-process-group sizes. ``--shard songs`` / ``--shard 2d
---song-groups G_s`` run those layouts as the main line (``--config c4`` /
-``c5`` for the full-scale configs).
+(1M train / 10k test / 384,546 songs, top-10) in the north star's layout —
+N song shards x 1 user block (sharding.ShardScorer, G_s = N: each rank the
+same whole number of wide tiles, its own co-listening index over its songs;
+ONE RCCL all-gather of the packed top-k record blocks per step, merged on the
+device), strong scaling over the fixed test set: slowest-rank ms per step,
+exchange ms, all-gather bytes, process-group sizes, the roofline of the route's
+encoding-independent byte model (split per kernel, beside SURVEY.md §8(d)'s
+two-hop bytes) and, at N = 1, the CPU two-hop baseline.
+Rank 0 builds C4 once and the node's other ranks load its arrays.
+``--shard songs`` / ``--shard 2d --song-groups G_s`` run those layouts as the
+main line (``--config c4`` / ``c5`` for the full-scale configs).
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the byte model.
 """
@@ -82,20 +85,42 @@ def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
 
 
 def cooc_bytes(eng, ds, out_bytes: int = 4, k: int = 10):
-    """Byte model of the ItemBasedModel's co-listening route (DESIGN.md §4),
-    from the engine's counts of the last ibm run (mr_cooc_stats):
-      build    4 Σ_rows (c_tr(s2) + Σ_{v∈L_tr(s2)} |S(v) ∩ shard|)   read each index row's
-               listeners and their songs once (4-B ids)
-               + 4 nnz(index)                                        write the index (4-B entries)
-      score    4 Σ_u Σ_{s2∈T(u)} nnz(row s2)                          read u's rows
-               + per user 4 n_s + out_bytes (n_s − |T(u)|)            scales + dense row
-      merge    12 k per user"""
-    index_nnz, consumed, build_reads = eng.cooc_stats()
+    """Byte model of the ItemBasedModel's co-listening route (DESIGN.md §4b),
+    encoding-independent, from the engine's counts of the last ibm run
+    (mr_cooc_bytes), split by kernel. Index segment (row s2, tile t) =
+    min(4 nnz(s2, t), songs of t) bytes: the cheaper exact encoding (4-B
+    entries or a count byte per song), whatever the build wrote.
+      build_heavy  4 Σ_heavy rows (c_tr(s2) + Σ_{v∈L_tr(s2)} |S(v) ∩ shard|)   listener lists
+                   and their shard rows read once (4-B ids) + the rows' index segments written
+      build_light  the same over the light rows (k_cooc_light*)
+      score        Σ_u Σ_{s2∈T(u)} Σ_t segment(s2, t)                        u's rows read
+                   + per user 4 n_s + out_bytes (n_s − heard in the shard)  scales + dense row
+      merge        12 k per user"""
+    b = eng.cooc_bytes()
     n_s = eng.width
-    te_n = np.diff(ds.te_off)
-    return {"build": 4 * build_reads + 4 * index_nnz,
-            "score": 4 * consumed + int(4 * n_s * ds.n_test + out_bytes * (n_s * ds.n_test - te_n.sum())),
+    heard = int(((ds.te_songs >= eng.song_lo) & (ds.te_songs < eng.song_hi)).sum())
+    return {"build_heavy": 4 * b["heavy_reads"] + b["heavy_index_bytes"],
+            "build_light": 4 * b["light_reads"] + b["light_index_bytes"],
+            "score": b["consumed_bytes"] + 4 * n_s * ds.n_test + out_bytes * (n_s * ds.n_test - heard),
             "merge": 12 * k * ds.n_test}
+
+
+def dataset_signature(ds):
+    """Sizes identifying a generated dataset (cached byte models are keyed by it)."""
+    return {"n_train": int(ds.n_train), "n_test": int(ds.n_test), "n_songs": int(ds.n_songs),
+            "nnz_train": int(ds.tr_off[-1]), "nnz_test": int(ds.te_off[-1])}
+
+
+def cached_twohop_bytes(cfg: str, ds):
+    """SURVEY.md §8(d)'s two-hop bytes of a full-scale config, top-k only, from
+    profiles/<cfg>_twohop_bytes.json (scripts/twohop_bytes.py) when its
+    dataset signature matches; else None."""
+    path = os.path.join(ROOT, "profiles", f"{cfg}_twohop_bytes.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return d if d.get("signature") == dataset_signature(ds) else None
 
 
 def kernel_bytes(ab, fused: bool):
@@ -372,6 +397,41 @@ def end_to_end(ds, model: str, reps: int = 3):
                     "D2H of the dense fp32 model; median of 3 (value excludes all of this but the kernels)"}
 
 
+def shared_bulk_dataset(cfg: str, world: int, rank: int):
+    """The full-scale dataset of every rank: at N > 1 rank 0 generates it once
+    (~20 s of numpy at C4) and writes its arrays to a node-local temporary
+    file that the other ranks load after a barrier (one process per GPU on ONE
+    node); returns (dataset, seconds)."""
+    import shutil
+    import tempfile
+
+    from musicrecommendation_amd.dataset import Dataset
+
+    t0 = time.perf_counter()
+    if world == 1:
+        return synth.config(cfg).dataset(), time.perf_counter() - t0
+    path = [None]
+    full = None
+    if rank == 0:
+        full = synth.config(cfg).dataset()
+        d = tempfile.mkdtemp(prefix=f"mr_{cfg}_", dir=os.environ.get("TMPDIR", "/tmp"))
+        full.save_arrays(os.path.join(d, "ds.npz"))
+        path = [d]
+    dist.broadcast_object_list(path, src=0)
+    if rank != 0:
+        full = Dataset.load_arrays(os.path.join(path[0], "ds.npz"))
+    dist.barrier()
+    if rank == 0:
+        shutil.rmtree(path[0], ignore_errors=True)
+    return full, time.perf_counter() - t0
+
+
+def host_peak_rss_gb() -> float:
+    import resource
+
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2 ** 20  # KiB -> GiB
+
+
 def north_star(args, world: int, rank: int, local: int):
     """The north star's layout at this N (BASELINE.json: "item-item similarity
     partitions by song-id range across the 8 GPUs ... with a single RCCL
@@ -385,26 +445,38 @@ def north_star(args, world: int, rank: int, local: int):
     blocks would each rebuild the popular rows) — and the shards exchange
     their top-k record blocks with ONE all-gather (RCCL) and merge them on the
     device (distributed.scala:477-479's song partition). Every rank runs this;
-    returns the block for rank 0's line (None elsewhere)."""
+    returns the block for rank 0's line (None elsewhere).
+
+    Roofline: the route's encoding-independent byte model (cooc_bytes, summed
+    over the ranks' shards, + the exchange's merge) over the slowest rank's
+    device time per step (HIP events on each engine stream), against N x 8 TB/s;
+    SURVEY.md §8(d)'s two-hop bytes beside it (profiles/c4_twohop_bytes.json).
+    At N = 1 the measured traffic (profiles/pmc_c4.json, same route) and the
+    CPU two-hop baseline (oracle/fixedpoint.c, the usable host cores, after the
+    timed region)."""
     from musicrecommendation_amd.sharding import ShardScorer
 
-    t0 = time.perf_counter()
-    full = synth.config("c4").dataset()
-    gen_s = time.perf_counter() - t0
+    full, gen_s = shared_bulk_dataset("c4", world, rank)
     gs = world
     t0 = time.perf_counter()
     scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32",
                          ibm_route=args.ibm_route)
     load_s = time.perf_counter() - t0
+    free_b, total_b = torch.cuda.mem_get_info(scorer.device)
+    eng = scorer.engine
 
-    def timed(fn, k):
+    def timed(fn, k, window=False):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         scorer.sync()
         t = time.perf_counter()
+        if window:
+            eng.timing_begin()
         for _ in range(k):
             fn()
+        if window:
+            eng.timing_stop()
         scorer.sync()
         torch.cuda.synchronize()
         if world > 1:
@@ -416,24 +488,75 @@ def north_star(args, world: int, rank: int, local: int):
 
     for _ in range(args.ns_warmup):
         scorer.step(args.model)
-    step_s = timed(lambda: scorer.step(args.model), args.ns_steps)
+    step_s = timed(lambda: scorer.step(args.model), args.ns_steps, window=True)
+    _n, win_ms = eng.timing_end()  # this rank's engine-stream time over the timed steps
     exch_s = timed(scorer.exchange, args.ns_steps) if scorer.gs > 1 else 0.0
-    pairs_rank = torch.tensor([float(scorer.pairs())], dtype=torch.float64, device="cuda")
+    cooc = args.model == "ibm" and eng.ibm_route == "cooc"
+    split = cooc_bytes(eng, scorer.ds, 0, 10) if cooc else {}
+    if cooc and scorer.gs > 1:  # the exchange's merge: G_s gathered lists read, one written, per user
+        split["exchange_merge"] = 12 * 10 * scorer.ds.n_test * (scorer.gs + 1)  # this rank: G_s lists in, one out
+    keys = ["build_heavy", "build_light", "score", "merge", "exchange_merge"]
+    vec = [float(split.get(k_, 0)) for k_ in keys]
+    vec += [float(scorer.pairs()), win_ms / args.ns_steps, host_peak_rss_gb(), float(total_b - free_b)]
+    st = torch.tensor(vec, dtype=torch.float64, device="cuda")
     if world > 1:
-        dist.all_reduce(pairs_rank, op=dist.ReduceOp.SUM)
-    pairs = float(pairs_rank.item())
+        sums = st.clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        maxs = st.clone()
+        dist.all_reduce(maxs, op=dist.ReduceOp.MAX)
+        sums, maxs = sums.tolist(), maxs.tolist()
+    else:
+        sums = maxs = st.tolist()
+    nk = len(keys)
+    byte_split = {k_: int(v) for k_, v in zip(keys, sums[:nk]) if v}
+    pairs, dev_ms = sums[nk], maxs[nk + 1]
     out = None
     if rank == 0:
         ms = step_s / args.ns_steps * 1e3
+        step_bytes = sum(byte_split.values())
+        roof = None
+        if cooc and dev_ms > 0:
+            ach = step_bytes / (dev_ms * 1e-3) / 1e9
+            peak = HBM_PEAK_GBS * world
+            traffic = traffic_src = None
+            pmc_file = os.path.join(ROOT, "profiles", "pmc_c4.json")
+            if world == 1 and os.path.exists(pmc_file):
+                with open(pmc_file) as f:
+                    pmc = json.load(f)
+                if pmc.get("ibm_route") == "cooc" and pmc.get("layout", "1x1") == "1x1":
+                    traffic = pmc.get("traffic_bytes_per_launch")
+                    traffic_src = "profiles/pmc_c4.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, one C4 step)"
+            th = cached_twohop_bytes("c4", full)
+            roof = {
+                "bound": "hbm", "kernel": "whole step: k_cooc_build + k_cooc_light* + k_score_wide<cooc> + "
+                                          "k_topk_merge (+ the exchange's merge at N > 1)",
+                "byte_model": "co-listening route, encoding-independent: per (row, tile) segment min(4 nnz, "
+                              "tile songs) B; listener lists + their shard rows read once as 4-B ids "
+                              "(bench.cooc_bytes, mr_cooc_bytes), summed over the N shards",
+                "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
+                "traffic": traffic, "traffic_source": traffic_src,
+                "traffic_frac": traffic / (dev_ms * 1e-3) / 1e9 / peak if traffic else None,
+                "algorithmic_bytes_per_step": step_bytes, "bytes_per_kernel": byte_split,
+                "device_ms_per_step": dev_ms,
+                "timing": "HIP events on each rank's engine stream around the timed steps; max over ranks",
+                "survey_two_hop": ({"bytes_per_step": th["total_bytes"], "source": "profiles/c4_twohop_bytes.json "
+                                   "(scripts/twohop_bytes.py: SURVEY.md §8(d), top-10 only)",
+                                   "achieved_GBps": th["total_bytes"] / (dev_ms * 1e-3) / 1e9,
+                                   "frac": th["total_bytes"] / (dev_ms * 1e-3) / 1e9 / peak,
+                                   "note": "the survey's two-hop algorithm's bytes over the same time: the route "
+                                           "computes the same integer sums with fewer bytes (DESIGN.md §4b), so "
+                                           "this fraction may exceed 1"} if th else None),
+            }
         out = {
             "workload": f"c4: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} {full.n_train} train / "
                         f"{full.n_test} test / {full.n_songs} songs, top-10 only",
             "layout": f"songs{scorer.gs}xusers{scorer.gu}", "song_shards": scorer.gs, "user_blocks": scorer.gu,
-            "ibm_route": scorer.engine.ibm_route, "tiles_per_rank": scorer.engine.n_tiles,
-            "songs_per_rank": scorer.engine.width,
+            "ibm_route": eng.ibm_route, "tiles_per_rank": eng.n_tiles, "block_songs": eng.block_songs,
+            "songs_per_rank": eng.width,
             "value": pairs * args.ns_steps / step_s, "unit": "pairs/s", "scaling": "strong",
             "pairs_per_step": pairs, "steps": args.ns_steps, "warmup": args.ns_warmup,
             "ms_per_step": ms,  # slowest rank: max over ranks of the barrier-bracketed window
+            "device_ms_per_step": dev_ms,
             "exchange_ms_per_step": exch_s / args.ns_steps * 1e3 if scorer.gs > 1 else 0.0,
             "exchange": ("one all_gather_into_tensor of the top-k record blocks (int64 keys + int32 songs) per "
                          "step inside each user block, then k_topk_merge on the device" if scorer.gs > 1 else
@@ -444,10 +567,22 @@ def north_star(args, world: int, rank: int, local: int):
                               "world_size": dist.get_world_size() if world > 1 else 1,
                               "block_group_size": dist.get_world_size(scorer.group) if world > 1 else 1},
             "setup_s": {"dataset": gen_s, "shard_load": load_s},
+            "host": {"threads_per_rank": _usable_threads(), "peak_rss_gb_max_rank": maxs[nk + 2],
+                     "peak_rss_gb_sum": sums[nk + 2], "device_used_gb_after_load_max": maxs[nk + 3] / 2 ** 30},
+            "roofline": roof,
             "note": "strong scaling: the N=1 line runs the whole C4 step on one GPU; compare ms_per_step across N",
         }
-    scorer.engine.close()
+    eng.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # after the timed region
+        out["cpu_baseline"] = cpu_baseline_twohop(full, args.model, args.cpu_baseline_seconds)
+        out["vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
     return out
+
+
+def _usable_threads() -> int:
+    from musicrecommendation_amd.mr_par_info import usable_cores
+
+    return usable_cores()
 
 
 def end_to_end_bulk(trip, model: str, reps: int = 2, k: int = 10):
@@ -590,8 +725,12 @@ def main() -> None:
         # fixed test set; small configs: weak, 10 test users per GPU in total.
         from musicrecommendation_amd.sharding import ShardScorer
 
-        trip = synth.config(args.config, n_test=None if bulk else n_te * world)
-        full = trip.dataset()
+        if bulk and world > 1:  # built once on the node (rank 0), loaded by the other ranks
+            trip = None
+            full, _gen_s = shared_bulk_dataset(args.config, world, rank)
+        else:
+            trip = synth.config(args.config, n_test=None if bulk else n_te * world)
+            full = trip.dataset()
         scorer = ShardScorer(full, rank, world, local, song_groups=song_groups_for(args, world), topk=10,
                              out_dtype="f32", dense=dense_out, stage1=args.stage1, block_songs=args.block_songs,
                              ibm_route=args.ibm_route)

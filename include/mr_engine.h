@@ -177,6 +177,32 @@ int mr_route_info(const mr_ctx* ctx, int32_t* route, int32_t* n_rows, int64_t* p
  * (the counts are those of the latest ibm run). */
 int mr_cooc_stats(mr_ctx* ctx, int64_t* index_nnz, int64_t* consumed, int64_t* build_reads);
 
+/* Encoding-independent byte counts of the latest ibm run on the co-listening
+ * route, split by kernel (bench.py's north-star roofline; synchronous). The
+ * index segment of row r (song s2) in tile t is charged the cheaper of its two
+ * exact encodings, min(4 * nnz(r, t), songs of t) bytes: 4-B (song, count)
+ * entries or a count byte per song of the tile (whatever the build actually
+ * wrote; a dense segment is charged its tile's songs, exact under the build's
+ * rule nnz * 3 >= songs — a test override of that rule, MR_COOC_DENSE_DIV,
+ * can make it an over-count). Reads are counted in 4-B ids: a row's listener list and each
+ * listener's songs in the shard, once.
+ *   heavy_*  rows built by k_cooc_build (one listener walk per tile),
+ *   light_*  rows built by k_cooc_light / k_cooc_light_wave (one walk);
+ *   *_reads         Σ_rows (c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard|) ids,
+ *   *_index_bytes   Σ_rows Σ_t min(4 nnz(r, t), songs of t),
+ *   heavy_visits    Σ_heavy rows c_tr(s2) · n_tiles (listener-tile visits),
+ *   consumed_bytes  Σ_u Σ_{s2 ∈ T(u)} Σ_t min(4 nnz(r, t), songs of t): the
+ *                   segments the scoring kernel reads.
+ * MR_E_STATE unless the context is on route 2 and has run ibm since its load. */
+typedef struct mr_cooc_bytes_t {
+  int64_t heavy_rows, light_rows;
+  int64_t heavy_reads, light_reads;
+  int64_t heavy_index_bytes, light_index_bytes;
+  int64_t heavy_visits;
+  int64_t consumed_bytes;
+} mr_cooc_bytes_t;
+int mr_cooc_bytes(mr_ctx* ctx, mr_cooc_bytes_t* out);
+
 /* Host only, before any load: the song tile of the wide shape that a context
  * with these options would use for n_train_users x n_test_users (the widest
  * the LDS holds, or opt->block_songs when set; opt = NULL: the defaults), or

@@ -107,6 +107,12 @@ class MrView(ctypes.Structure):
     ]
 
 
+class MrCoocBytes(ctypes.Structure):
+    """mr_cooc_bytes_t: encoding-independent byte counts of the co-listening route."""
+    _fields_ = [(n, c_int64) for n in ("heavy_rows", "light_rows", "heavy_reads", "light_reads",
+                                       "heavy_index_bytes", "light_index_bytes", "heavy_visits", "consumed_bytes")]
+
+
 MR_COMB_LINEAR = 0
 MR_COMB_AGGREGATION = 1
 MR_COMB_STOCHASTIC = 2
@@ -129,6 +135,7 @@ SIGNATURES = {
     "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_route_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int64)]),
     "mr_cooc_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
+    "mr_cooc_bytes": (c_int, [c_void_p, POINTER(MrCoocBytes)]),
     "mr_shard_tile_songs": (c_int, [POINTER(MrOptions), c_int32, c_int32, POINTER(c_int32)]),
     "mr_shard_tile_songs_n": (c_int, [POINTER(MrOptions), c_int32, c_int32, c_int32, c_int32, POINTER(c_int32)]),
     "mr_run": (c_int, [c_void_p, c_int]),

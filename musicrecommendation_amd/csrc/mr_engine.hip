@@ -1575,11 +1575,15 @@ typedef unsigned u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Co-listening index entries: (tile-local song << kCoocCntBits) | count, so
 // tiles <= 32768 songs and counts < 131072 (mr_load checks both).
 constexpr int kCoocCntBits = 17;
-// seg_len of a dense segment (counts of every song of the tile, u16 / u32)
 // seg_len of a dense segment (<= -3): a byte per song of the tile, the count
 // saturated at the build's sat value (255), then -seg_len - 3 sparse entries
 // carrying each larger count's excess (count - sat) — the dense pass adds
-// min(count, sat) · q, the sparse walk the rest
+// min(count, sat) · q, the sparse walk the rest.
+// The ORDER of the entries inside a sparse segment or a dense segment's excess
+// tail is unspecified (LDS atomics place them: the touched-song list, the
+// excess counter, the light rows' hash order and tile cursors), so two builds
+// of the same index may differ byte for byte; every consumer sums the entries
+// (order-free integer adds), so the scores never do. Compare indexes as sets.
 constexpr int kCoocDenseTail = -3;
 __host__ __device__ inline int cooc_dense_words(int bw) { return ((bw + 3) / 4 + 3) & ~3; }
 constexpr int kCoocDenseDiv = 3;
@@ -2060,9 +2064,24 @@ __host__ __device__ constexpr int light_tier_slots(int t) { return 32768 >> t; }
 // a table of S slots holds a row whose entry bound is at most S * 4/5 (the
 // bound counts every listener's songs; the distinct ones are far fewer)
 __host__ __device__ constexpr long long light_bound_max(long long slots) { return slots * 4 / 5; }
+// k_cooc_light's LDS layout (byte offsets): the hash table, per-tile counts and
+// cursors, the listener descriptors (m_a: NT int64, m_pre: NT + 1 ints, padded
+// to a 16-B multiple) and the block scan's NT / 64 wave totals.
 template <int NT, int SMAX>
-__host__ __device__ inline int cooc_light_lds() {
-  return SMAX * 4 + 2 * kLightMaxTiles * 4 + NT * 12 + 16 * 4 + 16;
+struct LightLds {
+  static constexpr int tab = 0;
+  static constexpr int tcnt = tab + SMAX * 4;
+  static constexpr int tpos = tcnt + kLightMaxTiles * 4;
+  static constexpr int m_a = tpos + kLightMaxTiles * 4;
+  static constexpr int m_pre = m_a + NT * 8;
+  static constexpr int s_scan = m_pre + (NT + 4) * 4;
+  static constexpr int total = (s_scan + (NT / 64) * 4 + 15) & ~15;
+  static_assert(m_a % 8 == 0 && s_scan % 16 == 0, "k_cooc_light LDS alignment");
+  static_assert(s_scan >= m_pre + (NT + 1) * 4, "m_pre holds NT + 1 prefix entries");
+};
+template <int NT, int SMAX>
+__host__ __device__ constexpr int cooc_light_lds() {
+  return LightLds<NT, SMAX>::total;
 }
 
 // P16: two u16 counters per LDS word (rows with < 65536 listeners: half the
@@ -2217,12 +2236,13 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
 template <int NT, int SMAX>
 __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  unsigned* tab = reinterpret_cast<unsigned*>(smem_raw);
-  int* tcnt = reinterpret_cast<int*>(tab + SMAX);
-  int* tpos = tcnt + kLightMaxTiles;
-  long long* m_a = reinterpret_cast<long long*>(tpos + kLightMaxTiles);
-  int* m_pre = reinterpret_cast<int*>(m_a + NT);
-  int* s_scan = m_pre + NT + 16;
+  using Lay = LightLds<NT, SMAX>;
+  unsigned* tab = reinterpret_cast<unsigned*>(smem_raw + Lay::tab);
+  int* tcnt = reinterpret_cast<int*>(smem_raw + Lay::tcnt);
+  int* tpos = reinterpret_cast<int*>(smem_raw + Lay::tpos);
+  long long* m_a = reinterpret_cast<long long*>(smem_raw + Lay::m_a);
+  int* m_pre = reinterpret_cast<int*>(smem_raw + Lay::m_pre);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + Lay::s_scan);
   const int r = p.rows[blockIdx.x];
   const int tid = threadIdx.x;
   const int S = p.row_slots[r];
@@ -2528,8 +2548,8 @@ __global__ __launch_bounds__(kWideThreads) void k_topk_dense(DenseTopkParams p) 
 }
 
 // auto shape: wide from this many (test user x train user) pairs of work
-// (scripts/shape_sweep.py, profiles/r01_final/shape_sweep_user.txt: wide wins
-// from 500 x 256 and 2000 x 100, fused below 500 x 128 and 2000 x 32)
+// (scripts/shape_sweep.py, profiles/r01_final/shape_sweep.txt: at 500 train x
+// 256 test users wide 0.101 ms vs fused 0.112; C2's 500 x 10 stays fused)
 constexpr long long kWideMinUserPairs = 100000;
 
 // ---------------------------------------------------------------------------
@@ -2718,6 +2738,9 @@ struct mr_ctx {
   DevBuf<unsigned> pool;
   DevBuf<unsigned> row_nnz;        // per run: each index row's non-zeros over the shard
   std::vector<int32_t> row_users;  // test users whose T(u) holds the row's song
+  std::vector<int64_t> row_reads;  // per row: c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_bytes)
+  std::vector<int32_t> row_listeners;  // per row: c_tr(s2)
+  std::vector<uint8_t> row_light;  // per row: built by the light-row kernels
   long long build_reads = 0;       // Σ_r c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard| (mr_cooc_stats)
   bool cooc_ran = false;           // an ibm run on route 2 since the load (its row_nnz are current)
   hipStream_t side[2] = {nullptr, nullptr};  // light-row build streams (created with the context)
@@ -2746,7 +2769,8 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    row_users.clear(); build_reads = 0; cooc_ran = false;
+    row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
+    build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
     for (int& x : n_light_tier) x = 0;
     if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
@@ -3593,6 +3617,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->row_users.assign(row_song.size(), 0);
     for (size_t i = 0; i < (size_t)d->te_off[n_te]; ++i)
       if (te_row[i] >= 0) c->row_users[te_row[i]]++;
+    c->row_reads = row_reads;
+    c->row_listeners.resize(row_song.size());
+    for (size_t r = 0; r < row_song.size(); ++r) c->row_listeners[r] = col_tr[row_song[r]];
+    c->row_light.assign(row_song.size(), 0);
+    for (int32_t r : light_rows) c->row_light[r] = 1;
     c->n_heavy32 = n_heavy32;
     c->n_big16 = n_big16;
     c->tcap16 = tcap16;
@@ -3664,6 +3693,42 @@ int mr_cooc_stats(mr_ctx* c, int64_t* index_nnz, int64_t* consumed, int64_t* bui
   if (index_nnz) *index_nnz = tot;
   if (consumed) *consumed = use;
   if (build_reads) *build_reads = c->build_reads;
+  return MR_OK;
+}
+
+int mr_cooc_bytes(mr_ctx* c, mr_cooc_bytes_t* out) {
+  if (!c || !out) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded || c->ibm_route != 2) return fail(MR_E_STATE, "mr_cooc_bytes needs a context on ibm_route 2");
+  if (!c->cooc_ran) return fail(MR_E_STATE, "mr_cooc_bytes before an ibm run");
+  MR_HIP(hipSetDevice(c->opt.device));
+  const int nr = c->n_rows, nt = c->n_tiles;
+  std::vector<int32_t> len((size_t)std::max(1, nr) * nt, 0);
+  if (nr > 0)
+    MR_HIP(hipMemcpyAsync(len.data(), c->seg_len.p, (size_t)nr * nt * 4, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  mr_cooc_bytes_t b{};
+  for (int r = 0; r < nr; ++r) {
+    int64_t seg = 0;  // Σ_t min(4 nnz(r, t), songs of t)
+    for (int t = 0; t < nt; ++t) {
+      const int blo = c->song_lo + t * c->block_songs;
+      const int64_t bw = std::min(c->song_hi, blo + c->block_songs) - blo;
+      const int32_t l = len[(size_t)t * nr + r];
+      // a dense segment (l <= kCoocDenseTail) holds >= bw / dense_div >= bw / 4 non-zeros
+      seg += l >= 0 ? std::min<int64_t>(4 * (int64_t)l, bw) : bw;
+    }
+    if (c->row_light[r]) {
+      b.light_rows++;
+      b.light_reads += c->row_reads[r];
+      b.light_index_bytes += seg;
+    } else {
+      b.heavy_rows++;
+      b.heavy_reads += c->row_reads[r];
+      b.heavy_index_bytes += seg;
+      b.heavy_visits += (int64_t)c->row_listeners[r] * nt;
+    }
+    b.consumed_bytes += seg * c->row_users[r];
+  }
+  *out = b;
   return MR_OK;
 }
 

@@ -74,6 +74,7 @@ struct Rccl {
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  bool shared_devices = false;  // the test library's marker (several ranks per device)
 };
 
 // The library: MR_RCCL_LIB when set (tests/fake_rccl runs the multi-context
@@ -105,6 +106,9 @@ Rccl& rccl_at(const std::string& path) {
   r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
   r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+  // a test library (tests/fake_rccl) exports this marker; it alone accepts
+  // several communicator ranks on one device
+  r.shared_devices = dlsym(h, "mr_fake_rccl_shared_devices") != nullptr;
   r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.group_start && r.group_end && r.error_string;
   if (!r.ok) r.why = "the RCCL library lacks a required symbol";
   return r;
@@ -392,15 +396,16 @@ int mr_group_create(const mr_options* opt, const mr_group_options* gopt, mr_grou
   if (transport == MR_TRANSPORT_AUTO) transport = n_distinct > 1 ? MR_TRANSPORT_RCCL : MR_TRANSPORT_COPY;
   if (transport == MR_TRANSPORT_COPY && n_distinct > 1)
     return gfail(MR_E_INVALID, "COPY transport keeps every context on one device (%d devices given)", n_distinct);
-  // RCCL needs one distinct device per context; only a library named by
-  // MR_RCCL_LIB (tests/fake_rccl: the multi-context path on one GPU) may be
-  // handed shared devices — real RCCL is never asked for two ranks on one GPU.
-  if (transport == MR_TRANSPORT_RCCL && n_distinct != G && rccl_path().empty())
-    return gfail(MR_E_INVALID, "RCCL transport needs one distinct device per context (%d contexts, %d devices)", G,
-                 n_distinct);
+  // RCCL needs one distinct device per context; only a library that exports
+  // the test marker (tests/fake_rccl, loaded through MR_RCCL_LIB: the
+  // multi-context path on one GPU) may be handed shared devices — real RCCL,
+  // whatever path names it, is never asked for two ranks on one GPU.
   Rccl* R = nullptr;
   if (transport == MR_TRANSPORT_RCCL) {
     R = &rccl_at(rccl_path());
+    if (n_distinct != G && !(R->ok && R->shared_devices))
+      return gfail(MR_E_INVALID, "RCCL transport needs one distinct device per context (%d contexts, %d devices)", G,
+                   n_distinct);
     if (!R->ok) return gfail(MR_E_RCCL, "RCCL unavailable: %s", R->why.c_str());
   }
   mr_group* g = new mr_group();

@@ -23,13 +23,18 @@ namespace mr_par {
 
 // Cores this process may really use: the affinity mask, capped by a cgroup v2
 // CPU quota (on the GPU box hardware_concurrency() shows the whole machine
-// while the job gets a 16-core share). MR_THREADS overrides.
+// while the job gets a 16-core share), then shared with the other ranks of a
+// one-process-per-GPU launch on this node (torchrun's LOCAL_WORLD_SIZE: 8
+// ranks on a 16-core share get 2 threads each, not 16 each). MR_THREADS
+// overrides.
 inline int usable_cores() {
   static const int n = [] {
     if (const char* e = std::getenv("MR_THREADS")) {
       const int t = std::atoi(e);
       if (t > 0) return std::min(t, 256);
     }
+    int local_ranks = 1;
+    if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) local_ranks = std::max(1, std::atoi(e));
     int aff = (int)std::thread::hardware_concurrency();
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) == 0) aff = CPU_COUNT(&set);
@@ -43,6 +48,7 @@ inline int usable_cores() {
     }
     int t = aff > 0 ? aff : 1;
     if (quota > 0) t = std::min(t, quota);
+    t /= local_ranks;
     return std::max(1, std::min(t, 256));
   }();
   return n;

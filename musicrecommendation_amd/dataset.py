@@ -68,11 +68,13 @@ class _Corpus:
 
 
 class _Buffer:
-    """numpy view of native memory that keeps its owner alive (the array's base)."""
+    """Read-only numpy view of native memory that keeps its owner alive (the
+    array's base). Read-only: the corpus is shared by every view, so an
+    in-place edit would silently change them all — copy first to modify."""
 
     def __init__(self, owner, addr: int, n: int, dt: np.dtype):
         self._owner = owner
-        self.__array_interface__ = {"shape": (n,), "typestr": dt.str, "data": (addr, False), "version": 3}
+        self.__array_interface__ = {"shape": (n,), "typestr": dt.str, "data": (addr, True), "version": 3}
 
 
 class _Names:
@@ -287,6 +289,26 @@ class Dataset:
             train_names=lambda i: user_name_fn(int(tr_keys[i])),
             test_names=lambda i: user_name_fn(int(te_keys[i])),
         )
+
+    # ---- arrays on disk (one build shared by the ranks of a node) --------------
+    _ARRAYS = ("tr_off", "tr_songs", "te_off", "te_songs", "song_count", "tr_len", "te_len", "lab_off", "lab_songs")
+
+    def save_arrays(self, path: str) -> None:
+        """The interned arrays as one uncompressed .npz (names are not kept):
+        bench.py's multi-rank runs build the full-scale dataset once and the
+        other ranks of the node load it (Dataset.load_arrays)."""
+        sizes = np.array([self.n_train, self.n_test, self.n_songs, self.n_label_songs, self.n_extra_songs],
+                         dtype=np.int64)
+        np.savez(path, sizes=sizes, **{k: np.asarray(getattr(self, k)) for k in self._ARRAYS})
+
+    @staticmethod
+    def load_arrays(path: str) -> "Dataset":
+        """Dataset.save_arrays' file -> Dataset without names (no pickles:
+        allow_pickle=False)."""
+        with np.load(path, allow_pickle=False) as z:
+            n_tr, n_te, n_s, n_lab, n_extra = (int(x) for x in z["sizes"])
+            arrs = {k: z[k] for k in Dataset._ARRAYS}
+        return Dataset(n_train=n_tr, n_test=n_te, n_songs=n_s, n_label_songs=n_lab, n_extra_songs=n_extra, **arrs)
 
     # ---- export ---------------------------------------------------------------
     def write_tsv(self, train_path: str, test_path: str, labels_path: str) -> None:

@@ -113,6 +113,13 @@ class Engine:
         _lib.check(self._L.mr_cooc_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "mr_cooc_stats")
         return a.value, b.value, c.value
 
+    def cooc_bytes(self) -> dict:
+        """Encoding-independent byte counts of the latest ibm run on the
+        co-listening route, split heavy / light rows (mr_cooc_bytes)."""
+        b = _lib.MrCoocBytes()
+        _lib.check(self._L.mr_cooc_bytes(self._h, ctypes.byref(b)), "mr_cooc_bytes")
+        return {name: int(getattr(b, name)) for name, _t in _lib.MrCoocBytes._fields_}
+
     def sync(self) -> None:
         _lib.check(self._L.mr_sync(self._h), "mr_sync")
 

@@ -1,5 +1,6 @@
 """Usable host cores, the rule of csrc/mr_par.h (affinity mask capped by the
-cgroup v2 CPU quota; MR_THREADS overrides)."""
+cgroup v2 CPU quota, divided among torchrun's LOCAL_WORLD_SIZE ranks of this
+node; MR_THREADS overrides)."""
 from __future__ import annotations
 
 import os
@@ -16,4 +17,7 @@ def usable_cores() -> int:
             n = min(n, max(1, int(int(q) / int(per))))
     except (OSError, ValueError):
         pass
+    local = os.environ.get("LOCAL_WORLD_SIZE", "")
+    if local.isdigit() and int(local) > 1:
+        n //= int(local)
     return max(1, min(n, 256))

@@ -122,7 +122,7 @@ case ",$STEPS," in *,profc4cooc,*)
 esac
 # Rehearsal of the driver's N>1 command on one GPU (gloo, every rank on device 0;
 # the real runs use RCCL, one GPU per rank): the C2 line + its north_star block.
-for n in 2 4; do
+for n in 2 4 8; do
   case ",$STEPS," in *,rehearse$n,*)
     MR_BENCH_BACKEND=gloo MR_BENCH_DEVICE=0 PYTHONUNBUFFERED=1 run rehearse_n$n 900 python -m torch.distributed.run \
       --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n \

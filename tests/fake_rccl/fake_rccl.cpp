@@ -106,6 +106,10 @@ ncclResult_t flush() {
 
 extern "C" {
 
+// Marker the engine's group looks up (mr_group.cpp): only a library exporting
+// it may be handed several contexts on one device. Real RCCL does not.
+int mr_fake_rccl_shared_devices(void) { return 1; }
+
 ncclResult_t ncclCommInitAll(ncclComm_t* comm, int ndev, const int* devlist) {
   if (!comm || ndev < 1) return ncclInvalidArgument;
   auto c = std::make_shared<Clique>();

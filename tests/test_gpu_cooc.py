@@ -9,6 +9,7 @@ bit-identity with the fixed-point oracle (oracle/fixedpoint.c) and with the
 two-hop route, on every tile width, shard, k and launch.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -138,7 +139,7 @@ def test_topk_only_graph_and_repeats():
         assert np.array_equal(s, ts) and np.array_equal(k, tk)
 
 
-def test_cold_and_heavy_users(build_path):
+def cold_heavy_dataset():
     """Test users whose songs have no train listener (empty rows), a test user
     with hundreds of songs (several descriptor passes), and one-song users."""
     rng = np.random.default_rng(11)
@@ -152,7 +153,31 @@ def test_cold_and_heavy_users(build_path):
     te_u = np.concatenate([np.full(heavy.size, K), [K + 1], [K + 2], base.test_u])
     te_s = np.concatenate([heavy, cold, pop, base.test_s])
     t = synth.Triplets(base.train_u, base.train_s, te_u, te_s, base.label_u[:0], base.label_s[:0], base.alpha)
-    ds = t.dataset()
+    return t.dataset()
+
+
+def test_cold_and_heavy_users(build_path):
+    ds = cold_heavy_dataset()
+    check_route_exact(ds, k=10)
+    check_route_exact(ds, k=16, block_songs=4096)
+
+
+@pytest.mark.parametrize("counters", ["u16_pairs", "u32"])
+def test_dense_excess_on_every_tile(counters, monkeypatch):
+    """Regression test of the dc4df36 race (k_cooc_build's dense branch: a
+    shared LDS word reset while other waves still read it). Every heavy row is
+    built by k_cooc_build (no light rows), every tile segment is dense
+    (MR_COOC_DENSE_DIV=1000000) and every count above 1 spills into the excess
+    tail (MR_COOC_SAT=1), so the excess counter and the non-zero counter are
+    both live on every tile of every row; u16-pair and u32 counter kernels."""
+    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT"):
+        monkeypatch.delenv(key, raising=False)
+    monkeypatch.setenv("MR_COOC_LIGHT", "0")
+    monkeypatch.setenv("MR_COOC_DENSE_DIV", "1000000")
+    monkeypatch.setenv("MR_COOC_SAT", "1")
+    if counters == "u32":
+        monkeypatch.setenv("MR_COOC_DENSE32", "1")
+    ds = cold_heavy_dataset()
     check_route_exact(ds, k=10)
     check_route_exact(ds, k=16, block_songs=4096)
 
@@ -185,6 +210,8 @@ def test_cooc_stats_count_the_index(build_path):
         e.run("ibm")
         e.run("ubm")  # the counts stay those of the latest ibm run
         index_nnz, consumed, reads = e.cooc_stats()
+        cb = e.cooc_bytes()
+        bs, n_tiles = e.block_songs, e.n_tiles
     tr_rows = np.repeat(np.arange(ds.n_train), np.diff(ds.tr_off))
     A = sp.csr_matrix((np.ones(tr_rows.size, np.int64), (tr_rows, ds.tr_songs)), shape=(ds.n_train, ds.n_songs))
     c_tr = np.asarray(A.sum(axis=0)).ravel()
@@ -197,3 +224,20 @@ def test_cooc_stats_count_the_index(build_path):
     assert index_nnz == int(nnz_r.sum())
     assert consumed == int((nnz_r * users_r).sum())
     assert reads == int(c_tr[rows].sum() + (A[:, rows].T @ deg).sum())
+    # mr_cooc_bytes: per (row, tile) segment min(4 nnz, tile songs) bytes
+    tile_of = C.indices // bs
+    row_of = np.repeat(np.arange(rows.size), nnz_r)
+    seg_nnz = np.bincount(row_of * n_tiles + tile_of, minlength=rows.size * n_tiles).reshape(rows.size, n_tiles)
+    bw = np.minimum(bs, ds.n_songs - bs * np.arange(n_tiles))
+    seg_min = np.minimum(4 * seg_nnz, bw[None, :]).sum(axis=1)
+    assert cb["heavy_rows"] + cb["light_rows"] == rows.size
+    assert cb["heavy_reads"] + cb["light_reads"] == reads
+    if os.environ.get("MR_COOC_LIGHT") == "0":
+        assert cb["light_rows"] == 0 and cb["heavy_visits"] == int(c_tr[rows].sum()) * n_tiles
+    got_index = cb["heavy_index_bytes"] + cb["light_index_bytes"]
+    if os.environ.get("MR_COOC_DENSE_DIV") is None:  # the build's own dense rule: exact
+        assert got_index == int(seg_min.sum())
+        assert cb["consumed_bytes"] == int((seg_min * users_r).sum())
+    else:  # a test dense rule charges a sparse-enough dense segment its tile's songs
+        assert got_index >= int(seg_min.sum())
+        assert cb["consumed_bytes"] >= int((seg_min * users_r).sum())

@@ -90,28 +90,98 @@ def c5():
     return synth.config("c5").dataset()
 
 
-def test_c4_ibm_all_users_top10_exact_on_sample(c4):
+@pytest.fixture(scope="module")
+def c4_ibm_1x1(c4):
+    """C4 ItemBasedModel top-10 of every test user on ONE context over all
+    songs (auto route: the co-listening index, asserted), plus the sample of
+    users checked against the oracle."""
     ds = c4
     assert (ds.n_train, ds.n_test, ds.n_songs) == (1_009_318, 10_000, 384_546)
     with Engine(ds, topk=K, dense=False) as e:
         assert e.shape == "wide" and e.n_chunks > 1
+        # the north star's route at C4: auto must pick the co-listening index
+        # (it falls back to two-hop only when the pool exceeds half the free
+        # device memory, which would leave the route untested here)
+        assert e.ibm_route == "cooc", e.ibm_route
+        assert e.cooc_rows > 0
         e.run("ibm")
         songs, scores, keys = e.topk()
         batch = e.batch
-    assert 1 <= batch < ds.n_test  # several neighbour batches: their boundaries are sampled
-    _check_topk_properties(ds, songs, keys)
-    assert np.array_equal(scores, keys.view(np.float64))
     work = _stage1_work(ds)
     tlen = np.diff(ds.te_off)
     sample = {int(np.argmax(tlen)), int(np.argmax(work)), int(np.argmin(work)), int(np.argmin(tlen))}
     for b0 in range(0, ds.n_test, batch):
         sample |= {b0, min(b0 + batch, ds.n_test) - 1}
     sample |= set(np.random.default_rng(44).choice(ds.n_test, 6, replace=False).tolist())
+    return songs, scores, keys, sorted(sample)
+
+
+def test_c4_ibm_all_users_top10_exact_on_sample(c4, c4_ibm_1x1):
+    ds = c4
+    songs, scores, keys, sample = c4_ibm_1x1
+    _check_topk_properties(ds, songs, keys)
+    assert np.array_equal(scores, keys.view(np.float64))
     assert len(sample) >= 16
     for lo, hi in _ranges(sample):
         _, ts, tk = native.fp_model(ds, "ibm", user_lo=lo, user_hi=hi, k=K, dense=False)
         assert np.array_equal(songs[lo:hi], ts), (lo, hi)
         assert np.array_equal(keys[lo:hi], tk), (lo, hi)
+
+
+def test_c4_north_star_8x1_song_shards(c4, c4_ibm_1x1):
+    """The north star's configuration itself (BASELINE.json north_star,
+    DESIGN.md §6): C4 ItemBasedModel in 8 song shards x 1 user block — each
+    shard 3 wide tiles of 16,128 songs on the co-listening route — every
+    shard's slice built and run in turn on this one GPU (distributed.scala:477-479
+    song partition), its top-k record block copied into one gathered buffer
+    (what the single all-gather delivers), merged on the device
+    (mr_topk_merge_records_async) and on the host: every test user's list
+    bitwise equal to the one-context run, and to oracle/fixedpoint.c on the
+    sampled users."""
+    from musicrecommendation_amd.engine import merge_topk_host
+    from musicrecommendation_amd.sharding import shard_tile, song_shards
+
+    ds = c4
+    songs1, _sc1, keys1, sample = c4_ibm_1x1
+    G = 8
+    tile = shard_tile(ds.n_train, ds.n_test, n_songs=ds.n_songs, n_shards=G)
+    assert tile == 16128
+    shards = song_shards(ds, G, tile)
+    assert shards[0][0] == 0 and shards[-1][1] == ds.n_songs
+    assert all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
+    dev = torch.device("cuda", 0)
+    rec_bytes = None
+    g_rec = None
+    host_s, host_k = [], []
+    for g, (lo, hi) in enumerate(shards):
+        with Engine(ds, topk=K, dense=False, song_lo=lo, song_hi=hi) as e:
+            assert e.ibm_route == "cooc" and e.n_tiles == 3 and e.block_songs == tile, (g, e.ibm_route, e.n_tiles)
+            e.run("ibm")
+            s, _sc, k = e.topk()
+            valid = s >= 0
+            assert np.all((s[valid] >= lo) & (s[valid] < hi)), g
+            host_s.append(s)
+            host_k.append(k)
+            if g_rec is None:
+                rec_bytes = e.record_bytes()
+                g_rec = torch.zeros(G * rec_bytes // 8, dtype=torch.int64, device=dev)
+            e.copy_topk_record(g_rec.data_ptr() + g * rec_bytes, wait=True)
+            if g == G - 1:  # the exchange's merge on the last shard's GPU context
+                out_s = torch.empty((ds.n_test, K), dtype=torch.int32, device=dev)
+                out_k = torch.empty((ds.n_test, K), dtype=torch.int64, device=dev)
+                out_sc = torch.empty((ds.n_test, K), dtype=torch.float64, device=dev)
+                e.merge_topk_records(G, g_rec.data_ptr(), rec_bytes, out_s.data_ptr(), out_k.data_ptr(),
+                                     out_sc.data_ptr())
+                e.sync()
+                dev_s, dev_k, dev_sc = out_s.cpu().numpy(), out_k.cpu().numpy(), out_sc.cpu().numpy()
+    hs, _hsc, hk = merge_topk_host(np.stack(host_s), np.stack(host_k))
+    assert np.array_equal(hs, songs1) and np.array_equal(hk, keys1), "8x1 host merge != one context"
+    assert np.array_equal(dev_s, songs1) and np.array_equal(dev_k, keys1), "8x1 device merge != one context"
+    assert np.array_equal(dev_sc, keys1.view(np.float64))
+    for lo, hi in _ranges(sample[:8]):
+        _, ts, tk = native.fp_model(ds, "ibm", user_lo=lo, user_hi=hi, k=K, dense=False)
+        assert np.array_equal(dev_s[lo:hi], ts), (lo, hi)
+        assert np.array_equal(dev_k[lo:hi], tk), (lo, hi)
 
 
 def test_c4_ubm_top10_exact_on_sample(c4):

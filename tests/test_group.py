@@ -307,6 +307,23 @@ def test_multi_context_rccl_path_equals_one_context(layout, dense, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_real_rccl_by_path_keeps_the_distinct_device_check(monkeypatch):
+    """MR_RCCL_LIB naming the real librccl does not lift the 'one distinct
+    device per context' rule: only a library exporting the test marker
+    (tests/fake_rccl) may be handed two contexts on one GPU."""
+    import os
+
+    real = "/opt/rocm/lib/librccl.so.1"
+    if not os.path.exists(real):
+        pytest.skip("no librccl in this image")
+    monkeypatch.setenv("MR_RCCL_LIB", real)
+    ds = synth_fixture("tiny")[0]
+    with pytest.raises(_lib.EngineError) as e:
+        Group(ds, song_shards=2, transport="rccl")
+    assert e.value.code == _lib.MR_E_INVALID
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("layout", [(2, 1), (3, 1), (2, 2)])
 @pytest.mark.parametrize("transport", ["copy", "rccl"])
 def test_group_colistening_route_equals_one_context(layout, transport, monkeypatch):

@@ -117,3 +117,48 @@ def test_gloo_2d_layout_exchange(world, song_groups):
         assert np.array_equal(np.array(s), ts[a:b]) and np.array_equal(np.array(k), tk[a:b]), r
         covered[a:b] = True
     assert covered.all()
+
+
+def _worker_shared(rank, world, port, out):
+    """bench.shared_bulk_dataset: rank 0 builds the dataset once, the others
+    load its arrays after a barrier; the node-local file is removed."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+
+        ds, _s = bench.shared_bulk_dataset("small", world, rank)
+        out[rank] = {k: np.asarray(getattr(ds, k)).tolist() for k in ds._ARRAYS} | {
+            "sizes": [ds.n_train, ds.n_test, ds.n_songs, ds.n_label_songs, ds.n_extra_songs]}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_shared_bulk_dataset(tmp_path, monkeypatch):
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    world = 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker_shared, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    ds = synth.config("small").dataset()
+    for r in range(world):
+        assert res[r]["sizes"] == [ds.n_train, ds.n_test, ds.n_songs, ds.n_label_songs, ds.n_extra_songs]
+        for k in ds._ARRAYS:
+            assert np.array_equal(np.array(res[r][k]), np.asarray(getattr(ds, k))), (r, k)
+    assert list(tmp_path.iterdir()) == []  # rank 0 removed the shared file
+
+
+def test_usable_cores_shared_by_local_ranks(monkeypatch):
+    """Host pools per rank: the usable cores divided by LOCAL_WORLD_SIZE
+    (csrc/mr_par.h and its Python twin)."""
+    from musicrecommendation_amd.mr_par_info import usable_cores
+
+    monkeypatch.delenv("MR_THREADS", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    full = usable_cores()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert usable_cores() == max(1, full // 8)
+    monkeypatch.setenv("MR_THREADS", "3")
+    assert usable_cores() == 3
