@@ -2021,7 +2021,7 @@ struct CoocParams {
   // k_cooc_light: the shard's train rows (renumbered users, shard-local song ids)
   const long long* sr_off;
   const unsigned* sr_songs;
-  const int* row_slots;          // [n_rows] hash slots of a light row (power of 2)
+  const int* row_slots;          // [n_rows] a light row's hash slots | lane-group log2 (kLightGlogShift)
   int dense_div;                 // dense segment when non-zeros * dense_div >= tile songs (0: never)
   int force32;                   // 1: every heavy row as a >= 65536-listener row (tests: the saturated format)
   unsigned sat;                  // saturation of the dense count bytes (255; tests lower it)
@@ -2053,6 +2053,10 @@ constexpr unsigned kLightCntMask = (1u << kLightCntBits) - 1u;
 constexpr int kLightSlots = 32768;
 constexpr int kLightMaxTiles = 256;
 constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
+// row_slots of a light row as uploaded: the table's slots (a power of 2 <= 2^15)
+// | log2(lanes per listener) << kLightGlogShift (light_walk)
+constexpr int kLightGlogShift = 24;
+constexpr int kLightSlotsMask = (1 << kLightGlogShift) - 1;
 // Light rows run in the smallest of four table sizes that holds them (the
 // rows are latency-bound, so smaller tables = more workgroups per CU):
 // 4096 slots / 256 threads (7 per CU), 8192 / 512 (4), 16384 / 512 (2),
@@ -2064,20 +2068,15 @@ __host__ __device__ constexpr int light_tier_slots(int t) { return 32768 >> t; }
 // a table of S slots holds a row whose entry bound is at most S * 4/5 (the
 // bound counts every listener's songs; the distinct ones are far fewer)
 __host__ __device__ constexpr long long light_bound_max(long long slots) { return slots * 4 / 5; }
-// k_cooc_light's LDS layout (byte offsets): the hash table, per-tile counts and
-// cursors, the listener descriptors (m_a: NT int64, m_pre: NT + 1 ints, padded
-// to a 16-B multiple) and the block scan's NT / 64 wave totals.
+// k_cooc_light's LDS layout (byte offsets): the hash table, then the per-tile
+// counts and cursors of the emission.
 template <int NT, int SMAX>
 struct LightLds {
   static constexpr int tab = 0;
   static constexpr int tcnt = tab + SMAX * 4;
   static constexpr int tpos = tcnt + kLightMaxTiles * 4;
-  static constexpr int m_a = tpos + kLightMaxTiles * 4;
-  static constexpr int m_pre = m_a + NT * 8;
-  static constexpr int s_scan = m_pre + (NT + 4) * 4;
-  static constexpr int total = (s_scan + (NT / 64) * 4 + 15) & ~15;
-  static_assert(m_a % 8 == 0 && s_scan % 16 == 0, "k_cooc_light LDS alignment");
-  static_assert(s_scan >= m_pre + (NT + 1) * 4, "m_pre holds NT + 1 prefix entries");
+  static constexpr int total = tpos + kLightMaxTiles * 4;
+  static_assert(total % 16 == 0, "k_cooc_light LDS size");
 };
 template <int NT, int SMAX>
 __host__ __device__ constexpr int cooc_light_lds() {
@@ -2226,10 +2225,95 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
   }
 }
 
+// Insert one shard-local song into a light row's LDS hash table (packed
+// ((song + 1) << kLightCntBits) | count slots, open addressing, linear probing,
+// CAS insert; S = mask + 1 slots, hash = the top log2(S) bits of key * φ).
+__device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int sh, unsigned key) {
+  const unsigned tag = (key + 1u) << kLightCntBits;
+  unsigned h = (key * 2654435761u) >> sh;
+  for (;;) {
+    unsigned x = tab[h];
+    if (x == 0u) {
+      x = atomicCAS(&tab[h], 0u, tag | 1u);
+      if (x == 0u) return;
+    }
+    if ((x & ~kLightCntMask) == tag) {
+      atomicAdd(&tab[h], 1u);
+      return;
+    }
+    h = (h + 1u) & mask;
+  }
+}
+
+// A light row's listener walk, by listener: the n_lanes lanes form groups of
+// G = 2^glog lanes (G <= 64: a group never spans two waves); group i takes the
+// listeners i, i + n_lanes / G, ... of the row and its G lanes read the
+// listener's shard row (sr_songs[sr_off[v] .. sr_off[v + 1]), sorted, shard-
+// local ids) in 16-B chunks, lane j the chunks at 4j, 4j + 4G, ..., every
+// entry inserted. G is chosen per row on the host from its entries per
+// listener (mr_load: about 6 entries per lane). Software-pipelined: the next
+// listener's row bounds and the id after it are loaded while the current
+// row's first two chunks are inserted. No listener descriptors in LDS, no
+// block scans, no barriers — the flattened walk this replaced advanced every
+// lane through the chunk's descriptors one LDS read at a time, a serial chain
+// of ~NT / (entries per listener) reads per entry (C4 8x1: 12 entries per
+// listener, 1024-lane chunks, 3.0 ms for tier 0). sr_songs is padded by 4
+// entries, so a chunk's 16-B load never leaves the buffer.
+template <typename Ins>
+__device__ __forceinline__ void light_walk(int lane_id, int n_lanes, int glog, const int* lst, int n,
+                                           const long long* sr_off, const unsigned* sr_songs, Ins&& ins) {
+  const int G = 1 << glog;
+  const int grp = lane_id >> glog, j = lane_id & (G - 1);
+  const int step = n_lanes >> glog;
+  auto chunk = [&](long long x, long long b, u32x4_a4& c) -> int {
+    const long long m = b - x;
+    c = u32x4_a4{0u, 0u, 0u, 0u};
+    if (m <= 0) return 0;
+    c = *reinterpret_cast<const u32x4_a4*>(sr_songs + x);
+    return m >= 4 ? 4 : (int)m;
+  };
+  auto put = [&](const u32x4_a4& c, int m) {
+    if (m > 0) ins(c.x);
+    if (m > 1) ins(c.y);
+    if (m > 2) ins(c.z);
+    if (m > 3) ins(c.w);
+  };
+  long long a0 = 0, b0 = 0;
+  if (grp < n) {
+    const int v = lst[grp];
+    a0 = sr_off[v];
+    b0 = sr_off[v + 1];
+  }
+  int v1 = grp + step < n ? lst[grp + step] : -1;
+  for (int l = grp; l < n; l += step) {
+    u32x4_a4 c0, c1;
+    const long long x0 = a0 + 4 * j;
+    const int m0 = chunk(x0, b0, c0);
+    const int m1 = chunk(x0 + 4 * G, b0, c1);
+    long long a1 = 0, b1 = 0;
+    if (v1 >= 0) {
+      a1 = sr_off[v1];
+      b1 = sr_off[v1 + 1];
+    }
+    const int l2 = l + 2 * step;
+    const int v2 = l2 < n ? lst[l2] : -1;
+    put(c0, m0);
+    put(c1, m1);
+    for (long long x = x0 + 8 * G; x < b0; x += 4 * G) {
+      u32x4_a4 c;
+      const int m = chunk(x, b0, c);
+      put(c, m);
+    }
+    a0 = a1;
+    b0 = b1;
+    v1 = v2;
+  }
+}
+
 // Light index rows: one workgroup per row (instead of one per (row, tile)).
-// The row's listeners' whole shard rows (sr_off / sr_songs) are walked as one
-// flattened list into an LDS hash table of counts (open addressing, linear
-// probing, CAS insert), then the table is emitted tile by tile: per-tile
+// The row's listeners' whole shard rows (sr_off / sr_songs) are walked by
+// listener (light_walk: groups of lanes per listener) into an LDS hash table
+// of counts (light_insert), then the table is emitted tile by tile: per-tile
 // counts, their prefix -> the row's segment of every tile (seg_off / seg_len,
 // empty tiles included), entries placed by LDS cursors (order inside a
 // segment is arbitrary; the consumer's sums are order-free).
@@ -2240,12 +2324,9 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   unsigned* tab = reinterpret_cast<unsigned*>(smem_raw + Lay::tab);
   int* tcnt = reinterpret_cast<int*>(smem_raw + Lay::tcnt);
   int* tpos = reinterpret_cast<int*>(smem_raw + Lay::tpos);
-  long long* m_a = reinterpret_cast<long long*>(smem_raw + Lay::m_a);
-  int* m_pre = reinterpret_cast<int*>(smem_raw + Lay::m_pre);
-  int* s_scan = reinterpret_cast<int*>(smem_raw + Lay::s_scan);
   const int r = p.rows[blockIdx.x];
   const int tid = threadIdx.x;
-  const int S = p.row_slots[r];
+  const int S = p.row_slots[r] & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
   for (int i = tid; i < S; i += NT) tab[i] = 0u;
@@ -2254,52 +2335,10 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   const long long la = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
-  for (int c0 = 0; c0 < n; c0 += NT) {
-    long long a = 0;
-    int len = 0;
-    if (c0 + tid < n) {
-      const int v = lst[c0 + tid];
-      a = p.sr_off[v];
-      len = (int)(p.sr_off[v + 1] - a);
-    }
-    int total;
-    const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);  // (its barriers also order the zeroing)
-    m_a[tid] = a - pre;
-    m_pre[tid] = pre;
-    if (tid == 0) m_pre[min(NT, n - c0)] = total;
-    __syncthreads();
-    constexpr int U = 4;
-    int cur = -1, ce = 0;
-    long long co = 0;
-    for (int e0 = tid; e0 < total; e0 += U * NT) {
-      unsigned key[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int e = e0 + j * NT;
-        key[j] = ~0u;
-        if (e < total) {
-          while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_a[cur]; }
-          key[j] = p.sr_songs[co + e];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        if (key[j] == ~0u) continue;
-        const unsigned tag = (key[j] + 1u) << kLightCntBits;
-        unsigned h = (key[j] * 2654435761u) >> sh;
-        for (;;) {
-          unsigned x = tab[h];
-          if (x == 0u) {
-            x = atomicCAS(&tab[h], 0u, tag | 1u);
-            if (x == 0u) break;
-          }
-          if ((x & ~kLightCntMask) == tag) { atomicAdd(&tab[h], 1u); break; }
-          h = (h + 1u) & mask;
-        }
-      }
-    }
-    __syncthreads();  // the next chunk rewrites the listener descriptors
-  }
+  __syncthreads();  // the table and the tile counters are zero
+  light_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, p.sr_off, p.sr_songs,
+             [&](unsigned key) { light_insert(tab, mask, sh, key); });
+  __syncthreads();
   // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
   for (int i = tid; i < S; i += NT) {
@@ -2340,12 +2379,11 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
 }
 
 // The smallest light rows, one wave per row (kWaveRowsPerBlock rows per
-// workgroup, each wave with its own table, tile counters and listener
-// descriptors in LDS): the same walk, hash and emission as k_cooc_light with
-// wave scans instead of block scans and no workgroup barriers, so 28 rows per
-// CU are in flight instead of 7 (the rows are latency-bound).
+// workgroup, each wave with its own table and tile counters in LDS): the same
+// walk, hash and emission as k_cooc_light with wave scans and no workgroup
+// barriers, so 16 rows per CU are in flight (the rows are latency-bound).
 template <int SW>
-__host__ __device__ constexpr int cooc_wave_bytes() { return SW * 4 + 2 * kWaveMaxTiles * 4 + 64 * 8 + 68 * 4; }
+__host__ __device__ constexpr int cooc_wave_bytes() { return SW * 4 + 2 * kWaveMaxTiles * 4; }
 template <int SW>
 __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(CoocParams p, int n_launch) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -2353,13 +2391,11 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const int ri = blockIdx.x * kWaveRowsPerBlock + w;
   if (ri >= n_launch) return;  // the whole wave (no workgroup barrier below)
   unsigned char* base = smem_raw + (size_t)w * cooc_wave_bytes<SW>();
-  long long* m_a = reinterpret_cast<long long*>(base);
-  unsigned* tab = reinterpret_cast<unsigned*>(m_a + 64);
+  unsigned* tab = reinterpret_cast<unsigned*>(base);
   int* tcnt = reinterpret_cast<int*>(tab + SW);
   int* tpos = tcnt + kWaveMaxTiles;
-  int* m_pre = tpos + kWaveMaxTiles;
   const int r = p.rows[ri];
-  const int S = p.row_slots[r];
+  const int S = p.row_slots[r] & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);
   for (int i = lane; i < S; i += 64) tab[i] = 0u;
@@ -2368,53 +2404,9 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const long long la = p.trs_off[s2];
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
-  for (int c0 = 0; c0 < n; c0 += 64) {
-    long long a = 0;
-    int len = 0;
-    if (c0 + lane < n) {
-      const int v = lst[c0 + lane];
-      a = p.sr_off[v];
-      len = (int)(p.sr_off[v + 1] - a);
-    }
-    const int inc = wave_incl_scan(len);
-    const int pre = inc - len;
-    const int total = __shfl(inc, 63, 64);
-    wave_lds_sync();  // the previous chunk's readers are done with the descriptors
-    m_a[lane] = a - pre;
-    m_pre[lane] = pre;
-    if (lane == 0) m_pre[min(64, n - c0)] = total;
-    wave_lds_sync();
-    constexpr int U = 4;
-    int cur = -1, ce = 0;
-    long long co = 0;
-    for (int e0 = lane; e0 < total; e0 += U * 64) {
-      unsigned key[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int e = e0 + j * 64;
-        key[j] = ~0u;
-        if (e < total) {
-          while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_a[cur]; }
-          key[j] = p.sr_songs[co + e];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        if (key[j] == ~0u) continue;
-        const unsigned tag = (key[j] + 1u) << kLightCntBits;
-        unsigned h = (key[j] * 2654435761u) >> sh;
-        for (;;) {
-          unsigned x = tab[h];
-          if (x == 0u) {
-            x = atomicCAS(&tab[h], 0u, tag | 1u);
-            if (x == 0u) break;
-          }
-          if ((x & ~kLightCntMask) == tag) { atomicAdd(&tab[h], 1u); break; }
-          h = (h + 1u) & mask;
-        }
-      }
-    }
-  }
+  wave_lds_sync();  // the table and the tile counters are zero
+  light_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, p.sr_off, p.sr_songs,
+             [&](unsigned key) { light_insert(tab, mask, sh, key); });
   wave_lds_sync();
   const int bs = p.block_songs;
   for (int i = lane; i < S; i += 64) {
@@ -3427,6 +3419,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           int sl = 1024;
           while (light_bound_max(sl) < row_base[r]) sl <<= 1;
           row_slots[r] = sl;
+          // lanes per listener of light_walk: the largest power of 2 G <= 16
+          // with 6 G <= the row's shard entries per listener (>= 6 per lane)
+          const int64_t c = col_tr[row_song[r]];
+          const int64_t per = c > 0 ? (row_reads[r] - c) / c : 0;
+          int glog = 0;
+          while (glog < 4 && ((int64_t)6 << (glog + 1)) <= per) ++glog;
+          row_slots[r] |= glog << kLightGlogShift;
           light_rows.push_back((int32_t)r);
           row_base[r] = (row_base[r] + 3) & ~(int64_t)3;
         } else {
@@ -3534,7 +3533,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
     // heavy rows, then light rows with large tables, then the small-table ones
     std::stable_sort(light_rows.begin(), light_rows.end(), [&](int32_t x, int32_t y) {
-      return light_tier(row_slots[x], n_tiles) < light_tier(row_slots[y], n_tiles);
+      return light_tier(row_slots[x] & kLightSlotsMask, n_tiles) < light_tier(row_slots[y] & kLightSlotsMask, n_tiles);
     });
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
@@ -3551,7 +3550,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         }
       });
       so[n_tr] = mr_par::exclusive_scan(so.data(), (int64_t)n_tr);
-      mr_par::buffer<uint32_t> ss((size_t)std::max<int64_t>(1, so[n_tr]));
+      // + 4 zero entries: light_walk's 16-B chunk loads never leave the buffer
+      mr_par::buffer<uint32_t> ss((size_t)so[n_tr] + 4);
+      std::fill(ss.begin() + so[n_tr], ss.end(), 0u);
       mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
         for (int64_t v = a; v < b; ++v) {
           const int32_t* r0 = std::lower_bound(tr_songs + tr_off[v], tr_songs + tr_off[v + 1], lo);
@@ -3559,7 +3560,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         }
       });
       if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
-      if ((rc = dev_upload(c->sr_songs, ss.data(), (size_t)std::max<int64_t>(1, so[n_tr]), st))) return rc;
+      if ((rc = dev_upload(c->sr_songs, ss.data(), ss.size(), st))) return rc;
       MR_HIP(hipStreamSynchronize(st));  // so / ss die here
     }
   }
@@ -3631,7 +3632,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->sat = cooc_sat_opt();
     c->n_light = (int)light_rows.size();
     for (int& x : c->n_light_tier) x = 0;
-    for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r], n_tiles)]++;
+    for (int32_t r : light_rows) c->n_light_tier[light_tier(row_slots[r] & kLightSlotsMask, n_tiles)]++;
     for (int t = 0; t < kLightTiers; ++t)
       if (int rc2 = light_tier_call(t, nullptr, 0, nullptr, CoocParams{})) return rc2;
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
