@@ -190,9 +190,11 @@ int mr_cooc_stats(mr_ctx* ctx, int64_t* index_nnz, int64_t* consumed, int64_t* b
  *   light_*  rows built by k_cooc_light / k_cooc_light_wave (one walk);
  *   *_reads         Σ_rows (c_tr(s2) + Σ_{v ∈ L_tr(s2)} |S(v) ∩ shard|) ids,
  *   *_index_bytes   Σ_rows Σ_t min(4 nnz(r, t), songs of t),
- *   heavy_visits    Σ_heavy rows c_tr(s2) · n_tiles (listener-tile visits),
+ *   heavy_visits    Σ_heavy rows c_tr(s2) · walks (listener visits: one walk per
+ *                   tile, or per tile group of k_cooc_group),
  *   consumed_bytes  Σ_u Σ_{s2 ∈ T(u)} Σ_t min(4 nnz(r, t), songs of t): the
- *                   segments the scoring kernel reads.
+ *                   segments the scoring kernel reads,
+ *   group_tiles, n_groups  the heavy build's tile grouping.
  * MR_E_STATE unless the context is on route 2 and has run ibm since its load. */
 typedef struct mr_cooc_bytes_t {
   int64_t heavy_rows, light_rows;
@@ -200,6 +202,8 @@ typedef struct mr_cooc_bytes_t {
   int64_t heavy_index_bytes, light_index_bytes;
   int64_t heavy_visits;
   int64_t consumed_bytes;
+  int64_t group_tiles;  /* tiles per k_cooc_group pass (0: heavy rows per tile) */
+  int64_t n_groups;     /* walks per u16 heavy row: tile groups, or n_tiles */
 } mr_cooc_bytes_t;
 int mr_cooc_bytes(mr_ctx* ctx, mr_cooc_bytes_t* out);
 

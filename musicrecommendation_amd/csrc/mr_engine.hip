@@ -2030,6 +2030,11 @@ struct CoocParams {
   int n_big;                     // k_cooc_build: the first n_big rows of the launch one workgroup per
                                  //   (row, tile), each tile's segment at row_base + tile * tcap
   int tcap;                      //   (words per tile of those rows); the rest one workgroup per row
+  // k_cooc_group: per train user a record of urec_words u32 words — word 0 the
+  // user's first entry in sr_songs, then u16 starts (relative to it) of every
+  // tile's entries, tiles 0..n_tiles — and the tile groups (grp tiles each)
+  const unsigned* urec;
+  int urec_words, grp, n_grp;
 };
 
 template <bool P16>
@@ -2054,7 +2059,7 @@ constexpr int kLightSlots = 32768;
 constexpr int kLightMaxTiles = 256;
 constexpr int kLightMaxWidth = (1 << (32 - kLightCntBits)) - 2;
 // row_slots of a light row as uploaded: the table's slots (a power of 2 <= 2^15)
-// | log2(lanes per listener) << kLightGlogShift (light_walk)
+// | log2(lanes per listener) << kLightGlogShift (rows_walk)
 constexpr int kLightGlogShift = 24;
 constexpr int kLightSlotsMask = (1 << kLightGlogShift) - 1;
 // Light rows run in the smallest of four table sizes that holds them (the
@@ -2083,74 +2088,21 @@ __host__ __device__ constexpr int cooc_light_lds() {
   return LightLds<NT, SMAX>::total;
 }
 
-// P16: two u16 counters per LDS word (rows with < 65536 listeners: half the
-// LDS, twice the workgroups per CU), else one u32 counter per song.
-template <int NT, bool P16>
-__global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(CoocParams p) {
+// One finished tile of an index row (counters in LDS, count_of(i) = song i's
+// count, `total` non-zeros, the first `cap` of them listed in `touched`)
+// written at pool[off]: a dense segment (a count byte per song, saturated at
+// p.sat, then the excess entries) when total * dense_div >= bw, else a sparse
+// one (from the touched list when it holds every non-zero, else a song-ordered
+// compaction). Sets seg_off / seg_len of (tile, r); returns the segment's
+// words. Called by the whole workgroup (barriers inside); *s_tail is zero on
+// entry; the caller synchronises before the counters or s_scan are reused.
+template <int NT, typename CountOf>
+__device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int tile, int bw, long long off, int total,
+                                              const unsigned short* touched, int kCap, int* s_tail, int* s_scan,
+                                              CountOf&& count_of) {
   constexpr int NW = NT / 64;
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  const int bs = p.block_songs;
-  unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
-  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(cooc_words<P16>(bs) * 4));
-  int* s_nz = s_scan + 16;      // songs first touched in this tile
-  int* s_tail = s_scan + 17;    // excess entries of this tile's dense segment
-  unsigned short* touched = reinterpret_cast<unsigned short*>(s_scan + 16 + 8);
-  constexpr int kCap = cooc_list_cap<P16>();
-  auto count_of = [&](int i) -> unsigned {
-    if constexpr (P16) return (cnt[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
-    else return cnt[i];
-  };
-  // big rows: one workgroup per (row, tile) at a fixed offset; the others:
-  // one workgroup per row, its tiles in turn at a running offset
-  const int nbt = p.n_big * p.n_tiles;
-  const bool big = (int)blockIdx.x < nbt;
-  const int ri = big ? (int)blockIdx.x / p.n_tiles : p.n_big + ((int)blockIdx.x - nbt);
-  const int r = p.rows[ri];
-  const int t_begin = big ? (int)blockIdx.x - ri * p.n_tiles : 0;
-  const int t_end = big ? t_begin + 1 : p.n_tiles;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
-  stamp_rt(sb, 0);
-  const int s2 = p.row_song[r];
-  const long long a = p.trs_off[s2];
-  const int n = (int)(p.trs_off[s2 + 1] - a);
-  const int* lst = p.trs_users + a;
-  constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
-  auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int k = k0 + j * NT;
-      v[j] = k < n ? lst[k] : -1;
-      q[j] = 1u;
-    }
-  };
-  // the row's tiles one after another: its segments are laid out in tile
-  // order from row_base[r] (no reservation atomics; the capacity bound holds)
-  long long off = p.row_base[r] + (long long)t_begin * p.tcap;  // (t_begin = 0 unless big)
-  unsigned row_nz = 0u;
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int blo = p.song_lo + tile * bs;
-    const int bw = min(p.song_hi, blo + bs) - blo;
-    for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
-    if (tid == 0) { *s_nz = 0; *s_tail = 0; }
-    __syncthreads();
-    walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
-                                           [&](unsigned x, unsigned) {
-                                             bool first;
-                                             if constexpr (P16) {
-                                               const unsigned sh = (x & 1) << 4;
-                                               first = ((atomicAdd(&cnt[x >> 1], 1u << sh) >> sh) & 0xffffu) == 0u;
-                                             } else {
-                                               first = atomicAdd(&cnt[x], 1u) == 0u;
-                                             }
-                                             if (first) {
-                                               const int k = atomicAdd(s_nz, 1);
-                                               if (k < kCap) touched[k] = (unsigned short)x;
-                                             }
-                                           });
-    __syncthreads();
-    const int total = *s_nz;
     // Dense segment when at least a third of the tile's songs are non-zero:
     // a count byte per song (no index, no atomics on the consumer side; the
     // rare counts above sat carried by excess entries). Segments are whole
@@ -2215,6 +2167,76 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
         base += __popcll(m);
       }
     }
+    return words;
+}
+
+// P16: two u16 counters per LDS word (rows with < 65536 listeners: half the
+// LDS, twice the workgroups per CU), else one u32 counter per song.
+template <int NT, bool P16>
+__global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(CoocParams p) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int bs = p.block_songs;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(cooc_words<P16>(bs) * 4));
+  int* s_nz = s_scan + 16;      // songs first touched in this tile
+  int* s_tail = s_scan + 17;    // excess entries of this tile's dense segment
+  unsigned short* touched = reinterpret_cast<unsigned short*>(s_scan + 16 + 8);
+  constexpr int kCap = cooc_list_cap<P16>();
+  auto count_of = [&](int i) -> unsigned {
+    if constexpr (P16) return (cnt[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
+    else return cnt[i];
+  };
+  // big rows: one workgroup per (row, tile) at a fixed offset; the others:
+  // one workgroup per row, its tiles in turn at a running offset
+  const int nbt = p.n_big * p.n_tiles;
+  const bool big = (int)blockIdx.x < nbt;
+  const int ri = big ? (int)blockIdx.x / p.n_tiles : p.n_big + ((int)blockIdx.x - nbt);
+  const int r = p.rows[ri];
+  const int t_begin = big ? (int)blockIdx.x - ri * p.n_tiles : 0;
+  const int t_end = big ? t_begin + 1 : p.n_tiles;
+  const int tid = threadIdx.x;
+  long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  stamp_rt(sb, 0);
+  const int s2 = p.row_song[r];
+  const long long a = p.trs_off[s2];
+  const int n = (int)(p.trs_off[s2 + 1] - a);
+  const int* lst = p.trs_users + a;
+  constexpr int R = MR_COOC_R, kSeg = MR_WIDE_SEG;
+  auto load_list = [&](int k0, int (&v)[R], unsigned (&q)[R]) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int k = k0 + j * NT;
+      v[j] = k < n ? lst[k] : -1;
+      q[j] = 1u;
+    }
+  };
+  // the row's tiles one after another: its segments are laid out in tile
+  // order from row_base[r] (no reservation atomics; the capacity bound holds)
+  long long off = p.row_base[r] + (long long)t_begin * p.tcap;  // (t_begin = 0 unless big)
+  unsigned row_nz = 0u;
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int blo = p.song_lo + tile * bs;
+    const int bw = min(p.song_hi, blo + bs) - blo;
+    for (int i = tid; i < cooc_words<P16>(bw); i += NT) cnt[i] = 0u;
+    if (tid == 0) { *s_nz = 0; *s_tail = 0; }
+    __syncthreads();
+    walk_tile_lists<NT, R, kSeg, unsigned>(tid, n, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
+                                           [&](unsigned x, unsigned) {
+                                             bool first;
+                                             if constexpr (P16) {
+                                               const unsigned sh = (x & 1) << 4;
+                                               first = ((atomicAdd(&cnt[x >> 1], 1u << sh) >> sh) & 0xffffu) == 0u;
+                                             } else {
+                                               first = atomicAdd(&cnt[x], 1u) == 0u;
+                                             }
+                                             if (first) {
+                                               const int k = atomicAdd(s_nz, 1);
+                                               if (k < kCap) touched[k] = (unsigned short)x;
+                                             }
+                                           });
+    __syncthreads();
+    const int total = *s_nz;
+    const int words = cooc_emit_tile<NT>(p, r, tile, bw, off, total, touched, kCap, s_tail, s_scan, count_of);
     off += words;
     row_nz += (unsigned)total;
     __syncthreads();  // the next tile rezeroes the counters
@@ -2245,10 +2267,11 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
   }
 }
 
-// A light row's listener walk, by listener: the n_lanes lanes form groups of
+// An index row's listener walk, by listener: the n_lanes lanes form groups of
 // G = 2^glog lanes (G <= 64: a group never spans two waves); group i takes the
 // listeners i, i + n_lanes / G, ... of the row and its G lanes read the
-// listener's shard row (sr_songs[sr_off[v] .. sr_off[v + 1]), sorted, shard-
+// listener's entries sr_songs[a .. b) (range(v, a, b): the whole shard row
+// for light rows, a tile group's part of it for k_cooc_group; sorted, shard-
 // local ids) in 16-B chunks, lane j the chunks at 4j, 4j + 4G, ..., every
 // entry inserted. G is chosen per row on the host from its entries per
 // listener (mr_load: about 6 entries per lane). Software-pipelined: the next
@@ -2259,9 +2282,9 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
 // of ~NT / (entries per listener) reads per entry (C4 8x1: 12 entries per
 // listener, 1024-lane chunks, 3.0 ms for tier 0). sr_songs is padded by 4
 // entries, so a chunk's 16-B load never leaves the buffer.
-template <typename Ins>
-__device__ __forceinline__ void light_walk(int lane_id, int n_lanes, int glog, const int* lst, int n,
-                                           const long long* sr_off, const unsigned* sr_songs, Ins&& ins) {
+template <typename Range, typename Ins>
+__device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
+                                          const unsigned* sr_songs, Ins&& ins) {
   const int G = 1 << glog;
   const int grp = lane_id >> glog, j = lane_id & (G - 1);
   const int step = n_lanes >> glog;
@@ -2279,11 +2302,7 @@ __device__ __forceinline__ void light_walk(int lane_id, int n_lanes, int glog, c
     if (m > 3) ins(c.w);
   };
   long long a0 = 0, b0 = 0;
-  if (grp < n) {
-    const int v = lst[grp];
-    a0 = sr_off[v];
-    b0 = sr_off[v + 1];
-  }
+  if (grp < n) range(lst[grp], a0, b0);
   int v1 = grp + step < n ? lst[grp + step] : -1;
   for (int l = grp; l < n; l += step) {
     u32x4_a4 c0, c1;
@@ -2291,10 +2310,7 @@ __device__ __forceinline__ void light_walk(int lane_id, int n_lanes, int glog, c
     const int m0 = chunk(x0, b0, c0);
     const int m1 = chunk(x0 + 4 * G, b0, c1);
     long long a1 = 0, b1 = 0;
-    if (v1 >= 0) {
-      a1 = sr_off[v1];
-      b1 = sr_off[v1 + 1];
-    }
+    if (v1 >= 0) range(v1, a1, b1);
     const int l2 = l + 2 * step;
     const int v2 = l2 < n ? lst[l2] : -1;
     put(c0, m0);
@@ -2310,9 +2326,19 @@ __device__ __forceinline__ void light_walk(int lane_id, int n_lanes, int glog, c
   }
 }
 
+// range of rows_walk: listener v's whole shard row
+struct ShardRow {
+  const long long* off;
+  __device__ __forceinline__ void operator()(int v, long long& a, long long& b) const {
+    a = off[v];
+    b = off[v + 1];
+  }
+};
+__device__ __forceinline__ ShardRow shard_row(const CoocParams& p) { return ShardRow{p.sr_off}; }
+
 // Light index rows: one workgroup per row (instead of one per (row, tile)).
 // The row's listeners' whole shard rows (sr_off / sr_songs) are walked by
-// listener (light_walk: groups of lanes per listener) into an LDS hash table
+// listener (rows_walk: groups of lanes per listener) into an LDS hash table
 // of counts (light_insert), then the table is emitted tile by tile: per-tile
 // counts, their prefix -> the row's segment of every tile (seg_off / seg_len,
 // empty tiles included), entries placed by LDS cursors (order inside a
@@ -2336,8 +2362,8 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
   __syncthreads();  // the table and the tile counters are zero
-  light_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, p.sr_off, p.sr_songs,
-             [&](unsigned key) { light_insert(tab, mask, sh, key); });
+  rows_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+            [&](unsigned key) { light_insert(tab, mask, sh, key); });
   __syncthreads();
   // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
@@ -2405,8 +2431,8 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
   wave_lds_sync();  // the table and the tile counters are zero
-  light_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, p.sr_off, p.sr_songs,
-             [&](unsigned key) { light_insert(tab, mask, sh, key); });
+  rows_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+            [&](unsigned key) { light_insert(tab, mask, sh, key); });
   wave_lds_sync();
   const int bs = p.block_songs;
   for (int i = lane; i < S; i += 64) {
@@ -2439,6 +2465,130 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
       const int pos = atomicAdd(&tpos[t], 1);
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
+  }
+}
+
+// k_cooc_group: the heavy rows under 65536 listeners, a tile GROUP per pass —
+// grp tiles' u16 counters (two per LDS word) side by side in LDS, so one walk
+// of the row's listeners serves grp tiles. Each listener's entries of the
+// group are one contiguous run of its shard row (user-major sr_songs: the
+// songs ascend, so tiles do), found through the listener's record (urec: one
+// aligned line holds its base and every tile's start). k_cooc_build's walk
+// gathered, per (row, tile, listener), a toff pair and a tile segment from two
+// tile-major arrays: two whole lines for ~5 entries, 20 times per listener at
+// C4 (107 GB of fetches per step for ~6 GB of entries).
+constexpr int kGroupCap = 480;       // touched-list entries per tile
+constexpr int kMaxGroupTiles = 8;
+constexpr int kGroupThreads = 1024;
+__host__ __device__ inline int cooc_group_lds(int bs, int g) {
+  return align16(g * bs * 2) + (16 + 2 * kMaxGroupTiles) * 4 + g * kGroupCap * 2;
+}
+// range of rows_walk: listener v's entries of tiles [t0, t1)
+struct GroupRange {
+  const unsigned* rec;
+  int words, t0, t1;
+  __device__ __forceinline__ void operator()(int v, long long& a, long long& b) const {
+    const unsigned* q = rec + (size_t)v * words;
+    const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
+    const long long base = q[0];
+    a = base + st[t0];
+    b = base + st[t1];
+  }
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int bs = p.block_songs, G = p.grp, ng = p.n_grp;
+  const int width = p.song_hi - p.song_lo;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
+  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(G * bs * 2));
+  int* s_nz = s_scan + 16;                   // [grp] songs first touched per tile
+  int* s_tail = s_nz + kMaxGroupTiles;       // [grp] excess entries per dense tile
+  unsigned short* touched = reinterpret_cast<unsigned short*>(s_tail + kMaxGroupTiles);
+  const int tid = threadIdx.x;
+  // big rows (the first n_big): one workgroup per (row, group), a row's groups
+  // on one XCD (blocks are dealt round-robin over the 8 XCDs: slot k of XCD x
+  // takes row x + 8 (k / ng), group k % ng — the groups share the listeners'
+  // records in that XCD's L2); the other rows one workgroup each, every group
+  // in turn at a running pool offset
+  const int lin = blockIdx.x;
+  const int nbg = (p.n_big + 7) / 8 * 8 * ng;
+  const bool big = lin < nbg;
+  int ri, g_begin, g_end;
+  if (big) {
+    const int slot = lin >> 3;
+    ri = (lin & 7) + 8 * (slot / ng);
+    g_begin = slot % ng;
+    g_end = g_begin + 1;
+    if (ri >= p.n_big) return;
+  } else {
+    ri = p.n_big + (lin - nbg);
+    g_begin = 0;
+    g_end = ng;
+  }
+  const int r = p.rows[ri];
+  const int s2 = p.row_song[r];
+  const long long la = p.trs_off[s2];
+  const int n = (int)(p.trs_off[s2 + 1] - la);
+  const int* lst = p.trs_users + la;
+  const int glog = p.row_slots[r] >> kLightGlogShift;
+  long long off = p.row_base[r];
+  unsigned row_nz = 0u;
+  for (int gi = g_begin; gi < g_end; ++gi) {
+    const int t0 = gi * G, t1 = min(p.n_tiles, t0 + G);
+    const int lo0 = t0 * bs;  // shard-local first song of the group
+    const int gw = min(width, t1 * bs) - lo0;
+    for (int i = tid; i < (gw + 1) / 2; i += NT) cnt[i] = 0u;
+    if (tid < kMaxGroupTiles) {
+      s_nz[tid] = 0;
+      s_tail[tid] = 0;
+    }
+    __syncthreads();
+    rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs, [&](unsigned key) {
+      const unsigned x = key - (unsigned)lo0;
+      const unsigned sh = (x & 1u) << 4;
+      if (((atomicAdd(&cnt[x >> 1], 1u << sh) >> sh) & 0xffffu) == 0u) {
+        const int k = (int)(x / (unsigned)bs);
+        const int j = atomicAdd(&s_nz[k], 1);
+        if (j < kGroupCap) touched[k * kGroupCap + j] = (unsigned short)(x - (unsigned)(k * bs));
+      }
+    });
+    __syncthreads();
+    for (int k = 0; k < t1 - t0; ++k) {
+      const int tile = t0 + k;
+      const int bw = min(width, (tile + 1) * bs) - tile * bs;
+      const int total = s_nz[k];
+      const int cb = k * bs;  // tile k's first counter (bs is even: whole words)
+      const long long o = big ? p.row_base[r] + (long long)tile * p.tcap : off;
+      const int words = cooc_emit_tile<NT>(p, r, tile, bw, o, total, touched + k * kGroupCap, kGroupCap, s_tail + k,
+                                           s_scan, [&](int i) -> unsigned {
+                                             const int x = cb + i;
+                                             return (cnt[x >> 1] >> ((x & 1) << 4)) & 0xffffu;
+                                           });
+      off += words;
+      row_nz += (unsigned)total;
+      __syncthreads();  // s_scan is rewritten by the next tile; the counters by the next group
+    }
+  }
+  if (tid == 0 && row_nz) atomicAdd(&p.row_nnz[r], row_nz);
+}
+
+// The records of k_cooc_group, built once per load: one thread per train user
+// walks its sorted shard row and writes its base and the start of every tile.
+__global__ __launch_bounds__(256) void k_urec(const long long* sr_off, const unsigned* sr_songs, int n_tr, int n_tiles,
+                                              int bs, int words, unsigned* rec) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= n_tr) return;
+  const long long a = sr_off[v], b = sr_off[v + 1];
+  unsigned* q = rec + (size_t)v * words;
+  q[0] = (unsigned)a;
+  unsigned short* st = reinterpret_cast<unsigned short*>(q + 1);
+  long long x = a;
+  for (int t = 0; t <= n_tiles; ++t) {
+    const unsigned lim = (unsigned)t * (unsigned)bs;
+    while (x < b && sr_songs[x] < lim) ++x;
+    st[t] = (unsigned short)(t == n_tiles ? b - a : x - a);
   }
 }
 
@@ -2745,8 +2895,10 @@ struct mr_ctx {
   unsigned sat = 255;
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
-  DevBuf<long long> sr_off;        // light rows: the shard's train rows
+  DevBuf<long long> sr_off;        // light rows / k_cooc_group: the shard's train rows
   DevBuf<unsigned> sr_songs;
+  DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts
+  int grp = 0, n_grp = 0, urec_words = 0;
 
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
@@ -2761,6 +2913,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
+    urec.release(); grp = n_grp = urec_words = 0;
     row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -2852,6 +3005,13 @@ int merge_rows_opt() {
 // (MR_COOC_LIGHT=0: A/B experiments and tests; read at each mr_load).
 bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
+  return !(e && std::atoi(e) == 0);
+}
+// Heavy u16 rows by tile groups (k_cooc_group, default) or per tile
+// (MR_COOC_GROUP=0: k_cooc_build<512, true>; A/B experiments and tests; read
+// at each mr_load).
+bool cooc_group_opt() {
+  const char* e = std::getenv("MR_COOC_GROUP");
   return !(e && std::atoi(e) == 0);
 }
 // Light rows on side streams (default) or on the context stream
@@ -3345,6 +3505,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   std::vector<int32_t> heavy_rows, light_rows, row_slots;
   int dense_div = kCoocDenseDiv;
   int n_heavy32 = 0, n_big16 = 0, tcap16 = 0, tcap32 = 0;
+  int32_t max_shard_deg = 0;
+  int grp = 0, n_grp = 0, urec_words = 0;  // k_cooc_group (0: the per-tile k_cooc_build)
   std::vector<int64_t> row_reads;
   int64_t pool_cap = 0;
   {
@@ -3381,6 +3543,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           deg[v] = (int32_t)(std::lower_bound(r0, r1, hi) - std::lower_bound(r0, r1, lo));
         }
       });
+      for (int v = 0; v < n_tr; ++v) max_shard_deg = std::max(max_shard_deg, deg[v]);
       const int64_t nr = (int64_t)row_song.size();
       row_base.assign((size_t)nr + 1, 0);
       row_reads.assign((size_t)nr, 0);
@@ -3419,7 +3582,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           int sl = 1024;
           while (light_bound_max(sl) < row_base[r]) sl <<= 1;
           row_slots[r] = sl;
-          // lanes per listener of light_walk: the largest power of 2 G <= 16
+          // lanes per listener of rows_walk: the largest power of 2 G <= 16
           // with 6 G <= the row's shard entries per listener (>= 6 per lane)
           const int64_t c = col_tr[row_song[r]];
           const int64_t per = c > 0 ? (row_reads[r] - c) / c : 0;
@@ -3462,6 +3625,31 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       for (size_t i = 0; i < heavy_rows.size(); ++i)
         if ((int)i < n_heavy32 + n_big16)
           row_base[heavy_rows[i]] = (int64_t)n_tiles * ((int)i < n_heavy32 ? tcap32 : tcap16);
+      // The u16 heavy rows by tile groups (k_cooc_group) when the per-user
+      // records fit (one 128-B line: n_tiles <= 61, u16 starts: shard rows
+      // < 65536 songs): the widest group whose counters fit the LDS.
+      urec_words = 1 + (n_tiles + 2) / 2;
+      if (cooc_group_opt() && (int)heavy_rows.size() > n_heavy32 && urec_words <= 32 && max_shard_deg <= 65535) {
+        grp = std::min(n_tiles, kMaxGroupTiles);
+        while (grp > 0 && cooc_group_lds(bs, grp) > kLdsBytes) --grp;
+      }
+      if (grp > 0) {
+        int w2 = 1;
+        while (w2 < urec_words) w2 <<= 1;
+        urec_words = w2;
+        n_grp = (n_tiles + grp - 1) / grp;
+        // lanes per listener of rows_walk: ~6 entries of the group per lane
+        for (size_t i = n_heavy32; i < heavy_rows.size(); ++i) {
+          const int32_t r = heavy_rows[i];
+          const int64_t cr = col_tr[row_song[r]];
+          const int64_t per = cr > 0 ? (row_reads[r] - cr) / cr * grp / n_tiles : 0;
+          int glog = 0;
+          while (glog < 4 && ((int64_t)6 << (glog + 1)) <= per) ++glog;
+          row_slots[r] = glog << kLightGlogShift;
+        }
+      } else {
+        urec_words = 0;
+      }
       pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
       row_base[nr] = pool_cap;
       size_t free_b = 0, total_b = 0;
@@ -3539,8 +3727,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
     if ((rc = dev_upload(c->row_slots, row_slots.data(), row_slots.size(), st))) return rc;
-    if (!light_rows.empty()) {
-      // the shard's train rows, shard-local song ids (k_cooc_light's input)
+    if (!light_rows.empty() || grp > 0) {
+      // the shard's train rows, shard-local song ids (k_cooc_light's and
+      // k_cooc_group's input)
       std::vector<int64_t> so((size_t)n_tr + 1, 0);
       mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
         for (int64_t v = a; v < b; ++v) {
@@ -3550,7 +3739,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         }
       });
       so[n_tr] = mr_par::exclusive_scan(so.data(), (int64_t)n_tr);
-      // + 4 zero entries: light_walk's 16-B chunk loads never leave the buffer
+      // + 4 zero entries: rows_walk's 16-B chunk loads never leave the buffer
       mr_par::buffer<uint32_t> ss((size_t)so[n_tr] + 4);
       std::fill(ss.begin() + so[n_tr], ss.end(), 0u);
       mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
@@ -3561,6 +3750,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       });
       if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
       if ((rc = dev_upload(c->sr_songs, ss.data(), ss.size(), st))) return rc;
+      if (grp > 0) {  // k_cooc_group's per-user records (tile starts), on the device
+        if ((rc = dev_alloc(c->urec, (size_t)std::max(1, n_tr) * urec_words))) return rc;
+        hipLaunchKernelGGL(k_urec, dim3((std::max(1, n_tr) + 255) / 256), dim3(256), 0, st, c->sr_off.p,
+                           c->sr_songs.p, n_tr, n_tiles, bs, urec_words, c->urec.p);
+        MR_HIP(hipGetLastError());
+      }
       MR_HIP(hipStreamSynchronize(st));  // so / ss die here
     }
   }
@@ -3625,6 +3820,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     for (int32_t r : light_rows) c->row_light[r] = 1;
     c->n_heavy32 = n_heavy32;
     c->n_big16 = n_big16;
+    c->grp = grp;
+    c->n_grp = n_grp;
+    c->urec_words = urec_words;
+    if (grp > 0)
+      MR_HIP(hipFuncSetAttribute((const void*)k_cooc_group<kGroupThreads>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 cooc_group_lds(bs, grp)));
     c->tcap16 = tcap16;
     c->tcap32 = tcap32;
     c->dense_div = dense_div;
@@ -3725,10 +3926,14 @@ int mr_cooc_bytes(mr_ctx* c, mr_cooc_bytes_t* out) {
       b.heavy_rows++;
       b.heavy_reads += c->row_reads[r];
       b.heavy_index_bytes += seg;
-      b.heavy_visits += (int64_t)c->row_listeners[r] * nt;
+      // listener walks: one per tile (k_cooc_build), one per tile group (k_cooc_group: u16 rows)
+      const bool u32row = c->force32 || c->row_listeners[r] >= 65536;
+      b.heavy_visits += (int64_t)c->row_listeners[r] * (c->grp > 0 && !u32row ? c->n_grp : nt);
     }
     b.consumed_bytes += seg * c->row_users[r];
   }
+  b.group_tiles = c->grp;
+  b.n_groups = c->grp > 0 ? c->n_grp : nt;
   *out = b;
   return MR_OK;
 }
@@ -3846,7 +4051,20 @@ int run_cooc(mr_ctx* c) {
                          hp);
       MR_HIP(hipGetLastError());
     }
-    if (n16 > 0) {
+    if (n16 > 0 && c->grp > 0) {  // by tile groups: big rows per (row, group), the others per row
+      CoocParams hp = cp;
+      hp.rows = c->rows_order.p + n32;
+      hp.n_big = c->n_big16;
+      hp.tcap = c->tcap16;
+      hp.urec = c->urec.p;
+      hp.urec_words = c->urec_words;
+      hp.grp = c->grp;
+      hp.n_grp = c->n_grp;
+      const int nblk = (c->n_big16 + 7) / 8 * 8 * c->n_grp + (n16 - c->n_big16);
+      hipLaunchKernelGGL(k_cooc_group<kGroupThreads>, dim3(nblk), dim3(kGroupThreads),
+                         (size_t)cooc_group_lds(c->block_songs, c->grp), st, hp);
+      MR_HIP(hipGetLastError());
+    } else if (n16 > 0) {
       CoocParams hp = cp;
       hp.rows = c->rows_order.p + n32;
       hp.n_big = c->n_big16;

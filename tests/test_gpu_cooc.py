@@ -59,12 +59,17 @@ BUILD_PATHS = {
     "dense_tail": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE_DIV": "1000000", "MR_COOC_DENSE32": "1",
                    "MR_COOC_SAT": "2"},
     "mixed_tail": {"MR_COOC_LIGHT": "0", "MR_COOC_DENSE32": "1", "MR_COOC_SAT": "3"},
+    # heavy u16 rows per tile (k_cooc_build<512, true>) instead of by tile
+    # groups (k_cooc_group, the default whenever the per-user records fit)
+    "pertile": {"MR_COOC_LIGHT": "0", "MR_COOC_GROUP": "0"},
+    "pertile_dense16": {"MR_COOC_LIGHT": "0", "MR_COOC_GROUP": "0", "MR_COOC_DENSE_DIV": "1000000"},
 }
+COOC_ENV = ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT", "MR_COOC_GROUP")
 
 
 @pytest.fixture(params=list(BUILD_PATHS))
 def build_path(request, monkeypatch):
-    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT"):
+    for key in COOC_ENV:
         monkeypatch.delenv(key, raising=False)
     for key, val in BUILD_PATHS[request.param].items():
         monkeypatch.setenv(key, val)
@@ -162,17 +167,20 @@ def test_cold_and_heavy_users(build_path):
     check_route_exact(ds, k=16, block_songs=4096)
 
 
-@pytest.mark.parametrize("counters", ["u16_pairs", "u32"])
+@pytest.mark.parametrize("counters", ["u16_groups", "u16_pertile", "u32"])
 def test_dense_excess_on_every_tile(counters, monkeypatch):
     """Regression test of the dc4df36 race (k_cooc_build's dense branch: a
     shared LDS word reset while other waves still read it). Every heavy row is
     built by k_cooc_build (no light rows), every tile segment is dense
     (MR_COOC_DENSE_DIV=1000000) and every count above 1 spills into the excess
     tail (MR_COOC_SAT=1), so the excess counter and the non-zero counter are
-    both live on every tile of every row; u16-pair and u32 counter kernels."""
-    for key in ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT"):
+    both live on every tile of every row; the u16-pair counters by tile groups
+    (k_cooc_group) and per tile, and the u32 counter kernel."""
+    for key in COOC_ENV:
         monkeypatch.delenv(key, raising=False)
     monkeypatch.setenv("MR_COOC_LIGHT", "0")
+    if counters == "u16_pertile":
+        monkeypatch.setenv("MR_COOC_GROUP", "0")
     monkeypatch.setenv("MR_COOC_DENSE_DIV", "1000000")
     monkeypatch.setenv("MR_COOC_SAT", "1")
     if counters == "u32":
@@ -232,8 +240,9 @@ def test_cooc_stats_count_the_index(build_path):
     seg_min = np.minimum(4 * seg_nnz, bw[None, :]).sum(axis=1)
     assert cb["heavy_rows"] + cb["light_rows"] == rows.size
     assert cb["heavy_reads"] + cb["light_reads"] == reads
-    if os.environ.get("MR_COOC_LIGHT") == "0":
-        assert cb["light_rows"] == 0 and cb["heavy_visits"] == int(c_tr[rows].sum()) * n_tiles
+    if os.environ.get("MR_COOC_LIGHT") == "0":  # every row heavy: one walk per tile, or per tile group
+        walks = n_tiles if (cb["group_tiles"] == 0 or os.environ.get("MR_COOC_DENSE32") == "1") else cb["n_groups"]
+        assert cb["light_rows"] == 0 and cb["heavy_visits"] == int(c_tr[rows].sum()) * walks
     got_index = cb["heavy_index_bytes"] + cb["light_index_bytes"]
     if os.environ.get("MR_COOC_DENSE_DIV") is None:  # the build's own dense rule: exact
         assert got_index == int(seg_min.sum())
