@@ -1520,6 +1520,7 @@ __device__ __forceinline__ int block_excl_scan_nt(int x, int* total, int* sbuf) 
 template <int NT>
 struct WideLds {
   int acc, heard, cpre, s_scan, wk, ws, fk, fs, gm, total;
+  WideLds<1024> as_wide() const { return WideLds<1024>{acc, heard, cpre, s_scan, wk, ws, fk, fs, gm, total}; }
 };
 template <int NT>
 __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
@@ -1795,6 +1796,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       }
       if (tid == 0) m_pre[ns] = total;
       __syncthreads();
+      MR_STAMP(12);  // (the last descriptor pass's) descriptors ready
       if (nd > 0) {
         // 8 songs per thread per block of 8 * NT, every dense row summed in registers
         for (int b0 = 8 * tid; b0 < bw; b0 += 8 * NT) {
@@ -1834,6 +1836,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
         __syncthreads();  // the sparse walk's atomics may hit any song
       }
+      MR_STAMP(13);  // dense rows summed
       // 4 consecutive entries per thread and load (one 16-B load when they
       // lie in one segment, else entry by entry), U loads in flight
       constexpr int U = MR_COOC_U;
@@ -1877,6 +1880,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
               atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
       }
       __syncthreads();  // the next pass rewrites the descriptors
+      MR_STAMP(14);  // sparse segments walked
     }
   } else {
   // stage 2: R neighbours per thread in flight; each segment's first kSeg
@@ -2871,6 +2875,8 @@ struct mr_ctx {
   long long win_launches = 0;
   // co-listening route (mr_options.ibm_route, k_cooc_build)
   int ibm_route = 1;               // 1 two-hop, 2 co-listening index
+  int cooc_nt = 1024;              // threads of the co-listening scoring workgroups (MR_COOC_NT)
+  size_t cooc_score_lds = 0;
   int n_rows = 0, nseg = 0;
   long long pool_cap = 0;
   size_t cooc_lds = 0;
@@ -3010,6 +3016,13 @@ bool cooc_light_opt() {
 // Heavy u16 rows by tile groups (k_cooc_group, default) or per tile
 // (MR_COOC_GROUP=0: k_cooc_build<512, true>; A/B experiments and tests; read
 // at each mr_load).
+// Threads per co-listening scoring workgroup: 1024 (default) or 512
+// (MR_COOC_NT=512: with a narrower block_songs, two or three workgroups per
+// CU; A/B experiments, read at each mr_load).
+int cooc_nt_opt() {
+  const char* e = std::getenv("MR_COOC_NT");
+  return e && std::atoi(e) == 512 ? 512 : 1024;
+}
 bool cooc_group_opt() {
   const char* e = std::getenv("MR_COOC_GROUP");
   return !(e && std::atoi(e) == 0);
@@ -3106,7 +3119,13 @@ void pick_kernels(mr_ctx* c) {
       c->score_kernel[MODEL] = f64 ? k_score_wide<MODEL, double, kWideThreads, kMaxTopkLarge, false>
                                    : k_score_wide<MODEL, float, kWideThreads, kMaxTopkLarge, false>;
     if constexpr (MODEL == MR_IBM) {
-      if (c->ibm_route == 2) {
+      if (c->ibm_route == 2 && c->cooc_nt == 512) {
+        if (c->opt.topk == 10)
+          c->cooc_kernel = f64 ? k_score_wide<MR_IBM, double, 512, 10, true> : k_score_wide<MR_IBM, float, 512, 10, true>;
+        else
+          c->cooc_kernel = f64 ? k_score_wide<MR_IBM, double, 512, kMaxTopkLarge, true>
+                               : k_score_wide<MR_IBM, float, 512, kMaxTopkLarge, true>;
+      } else if (c->ibm_route == 2) {
         if (c->opt.topk == 10)
           c->cooc_kernel = f64 ? k_score_wide<MR_IBM, double, kWideThreads, 10, true>
                                : k_score_wide<MR_IBM, float, kWideThreads, 10, true>;
@@ -3784,6 +3803,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->fused = fused;
   c->shape = shape;
   c->ibm_route = route;
+  c->cooc_nt = cooc_nt_opt();
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
@@ -3803,8 +3823,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->n_rows = (int)row_song.size();
     c->pool_cap = pool_cap;
     // the score kernel's row descriptors (40 B each: sparse + dense views) in its top-k scratch
-    const WideLds<kWideThreads> WL = wide_lds<kWideThreads>(bs, k, n_chunks);
-    c->nseg = std::min(kWideThreads, (WL.total - WL.wk - 8) / 40);
+    const WideLds<kWideThreads> WL = c->cooc_nt == 512 ? wide_lds<512>(bs, k, n_chunks).as_wide()
+                                                       : wide_lds<kWideThreads>(bs, k, n_chunks);
+    c->cooc_score_lds = (size_t)WL.total;
+    c->nseg = std::min(c->cooc_nt, (WL.total - WL.wk - 8) / 40);
     if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
     c->cooc_lds = (size_t)cooc_build_lds<false>(bs);
     c->n_heavy = (int)heavy_rows.size();
@@ -3837,7 +3859,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     for (int t = 0; t < kLightTiers; ++t)
       if (int rc2 = light_tier_call(t, nullptr, 0, nullptr, CoocParams{})) return rc2;
     MR_HIP(hipFuncSetAttribute((const void*)c->cooc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c->score_lds));
+                               (int)c->cooc_score_lds));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->cooc_lds));
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_build<MR_COOC_NT16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4115,7 +4137,7 @@ int run_cooc(mr_ctx* c) {
     sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
     sp.stamps = y0 == 0 ? c->stamps.p : nullptr;  // diagnostic build: the first launch
     sp.topk_lists = c->opt.topk_lists;
-    hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(kWideThreads), c->score_lds, st, sp);
+    hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(c->cooc_nt), c->cooc_score_lds, st, sp);
     MR_HIP(hipGetLastError());
     if (k > 0 && c->n_tiles > 1) {
       MergeParams mp{c->n_tiles, k, k, (long long)c->n_tiles * k, (long long)k, (long long)k, c->cand_key.p,

@@ -112,6 +112,30 @@ case ",$STEPS," in *,cfgroute,*)
 esac
 # per-rank device time of C4 layouts, one rank at a time on this GPU: LAYOUTS="1x1,2x1,4x1,8x1"
 case ",$STEPS," in *,layouts,*) run layouts 900 python -u scripts/layout_probe.py ibm ${LAYOUTS:-1x1,2x1,4x1,8x1,2x4} ;; esac
+# layout probe under engine-option variants: PROBES="label:KEY=V,KEY2=V;label2:..." (LAYOUTS as above)
+case ",$STEPS," in *,probes,*)
+  IFS=';' read -ra specs <<< "${PROBES:-base:}"
+  for spec in "${specs[@]}"; do
+    label=${spec%%:*}; kv=${spec#*:}
+    envs=()
+    IFS=',' read -ra pairs <<< "$kv"
+    for x in "${pairs[@]}"; do [ -n "$x" ] && envs+=("$x"); done
+    run probe_$label 600 env "${envs[@]}" MR_PROBE_REPS=${REPS:-3} python -u scripts/layout_probe.py ibm ${LAYOUTS:-1x1,8x1}
+  done ;;
+esac
+# rocprofv3 kernel stats of C4 (1x1, co-listening route, 3 steps) under engine-option
+# variants: PROFS="label:KEY=V,KEY2=V;label2:" (env set before rocprofv3, never after --)
+case ",$STEPS," in *,profs,*)
+  export TMPDIR=/tmp
+  IFS=';' read -ra specs <<< "${PROFS:-base:}"
+  for spec in "${specs[@]}"; do
+    label=${spec%%:*}; kv=${spec#*:}
+    envs=()
+    IFS=',' read -ra pairs <<< "$kv"
+    for x in "${pairs[@]}"; do [ -n "$x" ] && envs+=("$x"); done
+    run prof_$label 600 env "${envs[@]}" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$label" -o p -- python3 "$ROOT/bench.py" --config ${PCFG:-c4} --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc
+  done ;;
+esac
 case ",$STEPS," in *,proflayouts,*)
   export TMPDIR=/tmp
   run prof_layouts 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_layouts" -o p -- python3 "$ROOT/scripts/layout_probe.py" ibm ${LAYOUTS:-8x1} ;;

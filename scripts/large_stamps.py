@@ -18,7 +18,14 @@ if os.environ.get("CONFIG"):  # e.g. CONFIG=c2 STAGE1=wide: a bench config inste
     n_tr, n_te = ds.n_train, ds.n_test
 else:
     ds = synth.generate_bulk(n_tr, n_te, 4).dataset()
-with Engine(ds, topk=10, dense=bool(os.environ.get("DENSE")), block_songs=block,
+lo, hi = 0, 0
+if os.environ.get("SHARD"):  # SHARD=g/G: song shard g of G (sharding.song_shards at the shard tile)
+    from musicrecommendation_amd.sharding import shard_tile, song_shards
+
+    g, G = (int(x) for x in os.environ["SHARD"].split("/"))
+    tile = shard_tile(ds.n_train, ds.n_test, n_songs=ds.n_songs, n_shards=G, block_songs=block)
+    lo, hi = song_shards(ds, G, tile)[g]
+with Engine(ds, topk=10, dense=bool(os.environ.get("DENSE")), block_songs=block, song_lo=lo, song_hi=hi,
             stage1=os.environ.get("STAGE1", "auto")) as e:
     e.run(model)
     e.sync()
@@ -43,7 +50,8 @@ span = end.max() - t0
 dur = end - rt[:, 0]
 print(f"{n_tr}/{n_te} {model}: tiles={tiles} WGs={live.sum()} kernel span {span / 1e3:.2f} ms; "
       f"sum(WG time)/256 = {dur.sum() / 256 / 1e3:.2f} ms")
-for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5),
+for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), (" cooc descr", 1, 12), (" cooc dense", 12, 13),
+                   (" cooc sparse", 13, 14), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5),
                    (" topk scan", 3, 6), (" topk wave", 6, 7), (" topk barrier", 7, 8), (" topk merge", 8, 4),
                    (" thr pass1", 3, 9), (" thr rank", 9, 10), (" thr pass2", 10, 11), (" thr select", 11, 4)):
     d = rt[:, b] - rt[:, a]

@@ -131,7 +131,7 @@ def test_c4_ibm_all_users_top10_exact_on_sample(c4, c4_ibm_1x1):
 def test_c4_north_star_8x1_song_shards(c4, c4_ibm_1x1):
     """The north star's configuration itself (BASELINE.json north_star,
     DESIGN.md §6): C4 ItemBasedModel in 8 song shards x 1 user block — each
-    shard 3 wide tiles of 16,128 songs on the co-listening route — every
+    shard 3 wide tiles (<= 16,128 songs) on the co-listening route — every
     shard's slice built and run in turn on this one GPU (distributed.scala:477-479
     song partition), its top-k record block copied into one gathered buffer
     (what the single all-gather delivers), merged on the device
@@ -155,7 +155,8 @@ def test_c4_north_star_8x1_song_shards(c4, c4_ibm_1x1):
     host_s, host_k = [], []
     for g, (lo, hi) in enumerate(shards):
         with Engine(ds, topk=K, dense=False, song_lo=lo, song_hi=hi) as e:
-            assert e.ibm_route == "cooc" and e.n_tiles == 3 and e.block_songs == tile, (g, e.ibm_route, e.n_tiles)
+            # 3 tiles per shard (mr_load balances them inside the shard: <= the shard tile)
+            assert e.ibm_route == "cooc" and e.n_tiles == 3 and e.block_songs <= tile, (g, e.ibm_route, e.n_tiles)
             e.run("ibm")
             s, _sc, k = e.topk()
             valid = s >= 0
