@@ -185,6 +185,17 @@ __device__ __forceinline__ void stamp_rt(long long* sb, int i) {
   if (sb && threadIdx.x == 0) sb[i] = (long long)__builtin_amdgcn_s_memrealtime();
 #endif
 }
+// the same from lane 0 of every wave (one index row per wave)
+__device__ __forceinline__ void stamp_rt_wave(long long* sb, int i) {
+#ifdef MR_STAMPS
+  if (sb && (threadIdx.x & 63) == 0) sb[i] = (long long)__builtin_amdgcn_s_memrealtime();
+#endif
+}
+__device__ __forceinline__ void stamp_val(long long* sb, int i, long long v, bool wave = false) {
+#ifdef MR_STAMPS
+  if (sb && (wave ? (threadIdx.x & 63) == 0 : threadIdx.x == 0)) sb[i] = v;
+#endif
+}
 #ifdef MR_STAMPS
 #define MR_STAMP(i) stamp_at(p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr, (i))
 #else
@@ -2039,6 +2050,7 @@ struct CoocParams {
   // tile's entries, tiles 0..n_tiles — and the tile groups (grp tiles each)
   const unsigned* urec;
   int urec_words, grp, n_grp;
+  long long* lstamps;            // diagnostic build: [light row of the launch][8] (k_cooc_light*)
 };
 
 template <bool P16>
@@ -2104,7 +2116,6 @@ template <int NT, typename CountOf>
 __device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int tile, int bw, long long off, int total,
                                               const unsigned short* touched, int kCap, int* s_tail, int* s_scan,
                                               CountOf&& count_of) {
-  constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
     // Dense segment when at least a third of the tile's songs are non-zero:
@@ -2146,7 +2157,10 @@ __device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int ti
         const unsigned x = touched[k];
         out[k] = (x << kCoocCntBits) | count_of((int)x);
       }
-    } else {  // song-ordered compaction: wave w owns songs [wb, we), offsets by ballots
+    } else {  // compaction: wave w owns songs [wb, we); its run of the segment is
+              // reserved by one LDS atomic (*s_tail is free here: no excess
+              // entries), so the waves' runs land in arrival order (order
+              // inside a segment is unspecified) and no workgroup barrier
       if (tid == 0) {
         p.seg_off[(size_t)tile * p.n_rows + r] = off;
         p.seg_len[(size_t)tile * p.n_rows + r] = total;
@@ -2158,11 +2172,9 @@ __device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int ti
         const int i = i0 + lane;
         nz += __popcll(__ballot(i < we && count_of(i) != 0u));
       }
-      if (lane == 0) s_scan[w] = nz;
-      __syncthreads();
       int base = 0;
-#pragma unroll
-      for (int x = 0; x < NW; ++x) base += x < w ? s_scan[x] : 0;
+      if (lane == 0 && nz > 0) base = atomicAdd(s_tail, nz);
+      base = __shfl(base, 0, 64);
       for (int i0 = wb; i0 < we; i0 += 64) {
         const int i = i0 + lane;
         const unsigned c = i < we ? count_of(i) : 0u;
@@ -2286,12 +2298,17 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
 // of ~NT / (entries per listener) reads per entry (C4 8x1: 12 entries per
 // listener, 1024-lane chunks, 3.0 ms for tier 0). sr_songs is padded by 4
 // entries, so a chunk's 16-B load never leaves the buffer.
+#ifndef MR_WALK_R
+#define MR_WALK_R 2  // listeners per lane group per iteration of rows_walk (loads issued together)
+#endif
 template <typename Range, typename Ins>
 __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
                                           const unsigned* sr_songs, Ins&& ins) {
+  constexpr int R = MR_WALK_R;
   const int G = 1 << glog;
   const int grp = lane_id >> glog, j = lane_id & (G - 1);
   const int step = n_lanes >> glog;
+  const int stride = step * R;  // listeners per iteration of all groups
   auto chunk = [&](long long x, long long b, u32x4_a4& c) -> int {
     const long long m = b - x;
     c = u32x4_a4{0u, 0u, 0u, 0u};
@@ -2305,28 +2322,54 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
     if (m > 2) ins(c.z);
     if (m > 3) ins(c.w);
   };
-  long long a0 = 0, b0 = 0;
-  if (grp < n) range(lst[grp], a0, b0);
-  int v1 = grp + step < n ? lst[grp + step] : -1;
-  for (int l = grp; l < n; l += step) {
-    u32x4_a4 c0, c1;
-    const long long x0 = a0 + 4 * j;
-    const int m0 = chunk(x0, b0, c0);
-    const int m1 = chunk(x0 + 4 * G, b0, c1);
-    long long a1 = 0, b1 = 0;
-    if (v1 >= 0) range(v1, a1, b1);
-    const int l2 = l + 2 * step;
-    const int v2 = l2 < n ? lst[l2] : -1;
-    put(c0, m0);
-    put(c1, m1);
-    for (long long x = x0 + 8 * G; x < b0; x += 4 * G) {
-      u32x4_a4 c;
-      const int m = chunk(x, b0, c);
-      put(c, m);
+  // iteration i: listeners grp + i * stride + r * step, r < R; the next
+  // iteration's row ranges and the one after's ids are loaded while this
+  // iteration's first chunks are inserted
+  long long a0[R], b0[R];
+  int v1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int l = grp + r * step, l1 = l + stride;
+    a0[r] = b0[r] = 0;
+    if (l < n) range(lst[l], a0[r], b0[r]);
+    v1[r] = l1 < n ? lst[l1] : -1;
+  }
+  for (int l0 = grp; l0 < n; l0 += stride) {
+    u32x4_a4 c[R][2];
+    int m[R][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const long long x0 = a0[r] + 4 * j;
+      m[r][0] = chunk(x0, b0[r], c[r][0]);
+      m[r][1] = chunk(x0 + 4 * G, b0[r], c[r][1]);
     }
-    a0 = a1;
-    b0 = b1;
-    v1 = v2;
+    long long a1[R], b1[R];
+    int v2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      a1[r] = b1[r] = 0;
+      if (v1[r] >= 0) range(v1[r], a1[r], b1[r]);
+      const int l2 = l0 + 2 * stride + r * step;
+      v2[r] = l2 < n ? lst[l2] : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      put(c[r][0], m[r][0]);
+      put(c[r][1], m[r][1]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      for (long long x = a0[r] + 4 * j + 8 * G; x < b0[r]; x += 4 * G) {
+        u32x4_a4 cc;
+        const int mm = chunk(x, b0[r], cc);
+        put(cc, mm);
+      }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      a0[r] = a1[r];
+      b0[r] = b1[r];
+      v1[r] = v2[r];
+    }
   }
 }
 
@@ -2356,6 +2399,8 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   int* tpos = reinterpret_cast<int*>(smem_raw + Lay::tpos);
   const int r = p.rows[blockIdx.x];
   const int tid = threadIdx.x;
+  long long* sb = p.lstamps ? p.lstamps + (size_t)blockIdx.x * 8 : nullptr;
+  stamp_rt(sb, 0);
   const int S = p.row_slots[r] & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
@@ -2366,9 +2411,11 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
   __syncthreads();  // the table and the tile counters are zero
+  stamp_rt(sb, 1);
   rows_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
             [&](unsigned key) { light_insert(tab, mask, sh, key); });
   __syncthreads();
+  stamp_rt(sb, 2);
   // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
   for (int i = tid; i < S; i += NT) {
@@ -2376,6 +2423,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
     if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
   }
   __syncthreads();
+  stamp_rt(sb, 3);
   if (tid < 64) {  // prefix over <= kLightMaxTiles tiles by one wave
     int run = 0;
     if (tid == 0) {
@@ -2406,6 +2454,11 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
   }
+  __syncthreads();
+  stamp_rt(sb, 4);
+  stamp_val(sb, 5, n);
+  stamp_val(sb, 6, S);
+  stamp_val(sb, 7, NT);
 }
 
 // The smallest light rows, one wave per row (kWaveRowsPerBlock rows per
@@ -2425,6 +2478,8 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   int* tcnt = reinterpret_cast<int*>(tab + SW);
   int* tpos = tcnt + kWaveMaxTiles;
   const int r = p.rows[ri];
+  long long* sb = p.lstamps ? p.lstamps + (size_t)ri * 8 : nullptr;
+  stamp_rt_wave(sb, 0);
   const int S = p.row_slots[r] & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);
@@ -2435,9 +2490,11 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
   wave_lds_sync();  // the table and the tile counters are zero
+  stamp_rt_wave(sb, 1);
   rows_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
             [&](unsigned key) { light_insert(tab, mask, sh, key); });
   wave_lds_sync();
+  stamp_rt_wave(sb, 2);
   const int bs = p.block_songs;
   for (int i = lane; i < S; i += 64) {
     const unsigned x = tab[i];
@@ -2470,6 +2527,11 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
   }
+  wave_lds_sync();
+  stamp_rt_wave(sb, 4);
+  stamp_val(sb, 5, n, true);
+  stamp_val(sb, 6, S, true);
+  stamp_val(sb, 7, 64, true);
 }
 
 // k_cooc_group: the heavy rows under 65536 listeners, a tile GROUP per pass —
@@ -2483,7 +2545,6 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
 // C4 (107 GB of fetches per step for ~6 GB of entries).
 constexpr int kGroupCap = 480;       // touched-list entries per tile
 constexpr int kMaxGroupTiles = 8;
-constexpr int kGroupThreads = 1024;
 __host__ __device__ inline int cooc_group_lds(int bs, int g) {
   return align16(g * bs * 2) + (16 + 2 * kMaxGroupTiles) * 4 + g * kGroupCap * 2;
 }
@@ -2537,6 +2598,8 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   const int n = (int)(p.trs_off[s2 + 1] - la);
   const int* lst = p.trs_users + la;
   const int glog = p.row_slots[r] >> kLightGlogShift;
+  long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  stamp_rt(sb, 0);
   long long off = p.row_base[r];
   unsigned row_nz = 0u;
   for (int gi = g_begin; gi < g_end; ++gi) {
@@ -2559,6 +2622,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
       }
     });
     __syncthreads();
+    if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
     for (int k = 0; k < t1 - t0; ++k) {
       const int tile = t0 + k;
       const int bw = min(width, (tile + 1) * bs) - tile * bs;
@@ -2574,8 +2638,13 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
       row_nz += (unsigned)total;
       __syncthreads();  // s_scan is rewritten by the next tile; the counters by the next group
     }
+    if (gi == g_begin) stamp_rt(sb, 2);  // the first group's tiles emitted
   }
   if (tid == 0 && row_nz) atomicAdd(&p.row_nnz[r], row_nz);
+  stamp_rt(sb, 4);
+  stamp_val(sb, 5, big ? 1 : 0);
+  stamp_val(sb, 6, n);
+  stamp_val(sb, 7, g_end - g_begin);
 }
 
 // The records of k_cooc_group, built once per load: one thread per train user
@@ -2900,11 +2969,13 @@ struct mr_ctx {
   int dense_div = 0, force32 = 0;  // k_cooc_build's dense-segment rule
   unsigned sat = 255;
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
+  size_t lstamp_off = 0;           //   and the light rows' (one slot block per light row, launch order)
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
   DevBuf<long long> sr_off;        // light rows / k_cooc_group: the shard's train rows
   DevBuf<unsigned> sr_songs;
   DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts
   int grp = 0, n_grp = 0, urec_words = 0;
+  int group_nt = 1024;             // threads per k_cooc_group workgroup (MR_COOC_GNT)
 
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
@@ -3022,6 +3093,20 @@ bool cooc_light_opt() {
 int cooc_nt_opt() {
   const char* e = std::getenv("MR_COOC_NT");
   return e && std::atoi(e) == 512 ? 512 : 1024;
+}
+// Tiles per k_cooc_group pass at most (MR_COOC_GRP; default: as many as the
+// LDS holds, up to kMaxGroupTiles): fewer tiles = fewer bytes of LDS per
+// workgroup, more workgroups per CU, more listener walks (A/B experiments).
+// Threads per k_cooc_group workgroup: 1024 (default) or 512 (MR_COOC_GNT=512:
+// with MR_COOC_GRP=2, two workgroups per CU; A/B experiments).
+int cooc_group_nt_opt() {
+  const char* e = std::getenv("MR_COOC_GNT");
+  return e && std::atoi(e) == 512 ? 512 : 1024;
+}
+int cooc_group_max_opt() {
+  const char* e = std::getenv("MR_COOC_GRP");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? v : kMaxGroupTiles;
 }
 bool cooc_group_opt() {
   const char* e = std::getenv("MR_COOC_GROUP");
@@ -3649,7 +3734,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // < 65536 songs): the widest group whose counters fit the LDS.
       urec_words = 1 + (n_tiles + 2) / 2;
       if (cooc_group_opt() && (int)heavy_rows.size() > n_heavy32 && urec_words <= 32 && max_shard_deg <= 65535) {
-        grp = std::min(n_tiles, kMaxGroupTiles);
+        grp = std::min(std::min(n_tiles, kMaxGroupTiles), cooc_group_max_opt());
         while (grp > 0 && cooc_group_lds(bs, grp) > kLdsBytes) --grp;
       }
       if (grp > 0) {
@@ -3845,9 +3930,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->grp = grp;
     c->n_grp = n_grp;
     c->urec_words = urec_words;
+    c->group_nt = cooc_group_nt_opt();
     if (grp > 0)
-      MR_HIP(hipFuncSetAttribute((const void*)k_cooc_group<kGroupThreads>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 cooc_group_lds(bs, grp)));
+      MR_HIP(hipFuncSetAttribute(c->group_nt == 512 ? (const void*)k_cooc_group<512> : (const void*)k_cooc_group<1024>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, cooc_group_lds(bs, grp)));
     c->tcap16 = tcap16;
     c->tcap32 = tcap32;
     c->dense_div = dense_div;
@@ -3873,10 +3959,14 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
 #ifdef MR_STAMPS
   // scoring workgroups' slots, then (co-listening route) 8 per k_cooc_build workgroup
   const size_t stamp_users = (size_t)std::max(batch, route == 2 ? std::min(n_te, 65528) : 0) + 8;
-  const size_t n_stamps = (size_t)n_tiles * stamp_users * kStampSlots + (size_t)heavy_rows.size() * n_tiles * 8;
+  // scoring workgroups, then 8 per build workgroup (per (row, tile) bound + slack for the
+  // group grid's padding), then 8 per light row
+  const size_t build_wgs = (size_t)heavy_rows.size() * n_tiles + 64 * (size_t)std::max(1, n_tiles);
+  const size_t n_stamps = (size_t)n_tiles * stamp_users * kStampSlots + build_wgs * 8 + light_rows.size() * 8;
   if ((rc = dev_alloc(c->stamps, n_stamps))) return rc;
   MR_HIP(hipMemsetAsync(c->stamps.p, 0, n_stamps * 8, st));
   c->bstamp_off = (size_t)n_tiles * stamp_users * kStampSlots;
+  c->lstamp_off = c->bstamp_off + build_wgs * 8;
 #endif
   MR_HIP(hipStreamSynchronize(st));  // host vectors die at return
   trace("upload");
@@ -4082,9 +4172,13 @@ int run_cooc(mr_ctx* c) {
       hp.urec_words = c->urec_words;
       hp.grp = c->grp;
       hp.n_grp = c->n_grp;
+      if (hp.stamps) hp.stamps += (size_t)n32 * c->n_tiles * 8;
       const int nblk = (c->n_big16 + 7) / 8 * 8 * c->n_grp + (n16 - c->n_big16);
-      hipLaunchKernelGGL(k_cooc_group<kGroupThreads>, dim3(nblk), dim3(kGroupThreads),
-                         (size_t)cooc_group_lds(c->block_songs, c->grp), st, hp);
+      const size_t glds = (size_t)cooc_group_lds(c->block_songs, c->grp);
+      if (c->group_nt == 512)
+        hipLaunchKernelGGL(k_cooc_group<512>, dim3(nblk), dim3(512), glds, st, hp);
+      else
+        hipLaunchKernelGGL(k_cooc_group<1024>, dim3(nblk), dim3(1024), glds, st, hp);
       MR_HIP(hipGetLastError());
     } else if (n16 > 0) {
       CoocParams hp = cp;
@@ -4105,6 +4199,7 @@ int run_cooc(mr_ctx* c) {
       if (c->n_light_tier[t] == 0) continue;
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + lr;
+      lp.lstamps = c->stamps.p ? c->stamps.p + c->lstamp_off + (size_t)(lr - c->n_heavy) * 8 : nullptr;
       hipStream_t ls = side ? c->side[t < 2 ? 0 : 1] : st;
       if (int rc2 = light_tier_call(t, ls, c->n_light_tier[t], &lp, lp)) return rc2;
       lr += c->n_light_tier[t];

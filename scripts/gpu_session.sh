@@ -94,6 +94,16 @@ case ",$STEPS," in *,c4var,*)
   done ;;
 esac
 # phase stamps of the wide / co-listening scoring kernel: LSTAMPS="1009318 2000 ibm"
+# build-phase stamps (light rows per tier, heavy-row workgroups): C4 1x1 and the 8x1 shard 0
+case ",$STEPS," in *,bstamps,*)
+  run bstamps_1x1 600 python -u scripts/cooc_build_stamps.py
+  SHARD=0/8 run bstamps_8x1 600 python -u scripts/cooc_build_stamps.py ;;
+esac
+# scoring-kernel phase stamps of the 8x1 shard 0 and of C4 1x1 (co-listening route)
+case ",$STEPS," in *,sstamps,*)
+  SHARD=0/8 run sstamps_8x1 600 python -u scripts/large_stamps.py 1009318 10000 ibm
+  run sstamps_1x1 600 python -u scripts/large_stamps.py 1009318 10000 ibm ;;
+esac
 case ",$STEPS," in *,cstamps,*) run cstamps 600 python -u scripts/cooc_stamps.py ${CSTAMPS:-} ;; esac
 case ",$STEPS," in *,lstamps,*) run lstamps 600 python -u scripts/large_stamps.py ${LSTAMPS:-1009318 2000 ibm} ;; esac
 # C4 ibm per wide-kernel block map (MR_WIDE_MAP): MAPS="1 2 3"
