@@ -2266,9 +2266,47 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
 // Insert one shard-local song into a light row's LDS hash table (packed
 // ((song + 1) << kLightCntBits) | count slots, open addressing, linear probing,
 // CAS insert; S = mask + 1 slots, hash = the top log2(S) bits of key * φ).
+#ifndef MR_LIGHT_INSERT
+#define MR_LIGHT_INSERT 1  // 1: 4-slot probes (one 16-B LDS read per step); 0: slot by slot;
+                           // 8, 9: timing-only stubs (wrong counts: no probing / a bare add)
+#endif
 __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int sh, unsigned key) {
   const unsigned tag = (key + 1u) << kLightCntBits;
   unsigned h = (key * 2654435761u) >> sh;
+#if MR_LIGHT_INSERT == 9
+  atomicAdd(&tab[h], 1u);
+  (void)tag;
+  (void)mask;
+#elif MR_LIGHT_INSERT == 8
+  unsigned x = tab[h];
+  if (x == 0u) x = atomicCAS(&tab[h], 0u, tag | 1u);
+  if (x != 0u) atomicAdd(&tab[h], 1u);
+  (void)mask;
+#elif MR_LIGHT_INSERT == 1
+  // linear probing over aligned groups of 4 slots, read 16 B at a time: the
+  // same probe order as slot by slot (home slot first, wrapping), so a key is
+  // always found before the first empty slot after its home; about a quarter
+  // of the dependent LDS reads on long clusters
+  unsigned g = h & ~3u;
+  int i = (int)(h & 3u);
+  for (;;) {
+    const uint4 q = *reinterpret_cast<const uint4*>(tab + g);
+    const unsigned v[4] = {q.x, q.y, q.z, q.w};
+    for (; i < 4; ++i) {
+      unsigned x = v[i];
+      if (x == 0u) {
+        x = atomicCAS(&tab[g + i], 0u, tag | 1u);
+        if (x == 0u) return;
+      }
+      if ((x & ~kLightCntMask) == tag) {
+        atomicAdd(&tab[g + i], 1u);
+        return;
+      }
+    }
+    g = (g + 4u) & mask;
+    i = 0;
+  }
+#else
   for (;;) {
     unsigned x = tab[h];
     if (x == 0u) {
@@ -2281,6 +2319,7 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
     }
     h = (h + 1u) & mask;
   }
+#endif
 }
 
 // An index row's listener walk, by listener: the n_lanes lanes form groups of
@@ -2543,10 +2582,90 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
 // gathered, per (row, tile, listener), a toff pair and a tile segment from two
 // tile-major arrays: two whole lines for ~5 entries, 20 times per listener at
 // C4 (107 GB of fetches per step for ~6 GB of entries).
-constexpr int kGroupCap = 480;       // touched-list entries per tile
 constexpr int kMaxGroupTiles = 8;
 __host__ __device__ inline int cooc_group_lds(int bs, int g) {
-  return align16(g * bs * 2) + (16 + 2 * kMaxGroupTiles) * 4 + g * kGroupCap * 2;
+  return align16(g * bs * 2) + 3 * kMaxGroupTiles * 4;  // counters; per tile: total, cursor, excess
+}
+
+// Non-zero u16 counters among the 8 of a 16-B chunk (songs song0 .. song0 + 7
+// of a tile of bw songs).
+__device__ __forceinline__ int nz_pairs8(const uint4& w, int song0, int bw) {
+  int n = 0;
+  const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) n += (song0 + i < bw && ((ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu)) ? 1 : 0;
+  return n;
+}
+
+// One tile of a k_cooc_group row written at pool[off] from its u16 counters
+// cw[0 .. bw) (two per word, 16-B aligned): the non-zeros counted from 16-B
+// chunks (8 counters per lane and LDS read, one LDS add per wave), then a dense
+// segment (count bytes + excess entries, as cooc_emit_tile) or a sparse one by
+// compaction — a lane's non-zeros placed at its wave's prefix from a DPP scan,
+// the wave's run reserved by one LDS add per chunk row (order inside the
+// segment unspecified). No per-entry bookkeeping during the walk: the walk's
+// adds are fire-and-forget. s_tot / s_cur / s_tail are zero on entry. Sets
+// seg_off / seg_len; returns (words, non-zeros). Called by the whole workgroup.
+template <int NT>
+__device__ __forceinline__ int2 cooc_emit_tile16(const CoocParams& p, int r, int tile, int bw, long long off,
+                                                 const unsigned* cw, int* s_tot, int* s_cur, int* s_tail) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int nch = (bw + 7) >> 3;
+  const uint4* cv = reinterpret_cast<const uint4*>(cw);
+  int nz = 0;
+  for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c], c * 8, bw);
+  const int wsum = __shfl(wave_incl_scan(nz), 63, 64);
+  if (lane == 0 && wsum) atomicAdd(s_tot, wsum);
+  __syncthreads();
+  const int total = *s_tot;
+  auto count_of = [&](int i) -> unsigned { return (cw[i >> 1] >> ((i & 1) << 4)) & 0xffffu; };
+  unsigned* out = p.pool + off;
+  int words = (total + 3) & ~3;
+  if (p.dense_div > 0 && (long long)total * p.dense_div >= bw) {
+    const int dwords = cooc_dense_words(bw);
+    for (int i = tid; 4 * i < bw; i += NT) {
+      unsigned wv = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = 4 * i + j;
+        const unsigned c = col < bw ? count_of(col) : 0u;
+        wv |= min(c, p.sat) << (8 * j);
+        if (c > p.sat) out[dwords + atomicAdd(s_tail, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
+      }
+      out[i] = wv;
+    }
+    __syncthreads();
+    const int tail = *s_tail;
+    words = (dwords + tail + 3) & ~3;
+    if (tid == 0) {
+      p.seg_off[(size_t)tile * p.n_rows + r] = off;
+      p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDenseTail - tail;
+    }
+  } else {
+    if (tid == 0) {
+      p.seg_off[(size_t)tile * p.n_rows + r] = off;
+      p.seg_len[(size_t)tile * p.n_rows + r] = total;
+    }
+    for (int c0 = 0; c0 < nch; c0 += NT) {  // wave-uniform trip count (scans inside)
+      const int c = c0 + tid;
+      uint4 w = make_uint4(0u, 0u, 0u, 0u);
+      if (c < nch) w = cv[c];
+      const int n = c < nch ? nz_pairs8(w, c * 8, bw) : 0;
+      const int incl = wave_incl_scan(n);
+      const int wtot = __shfl(incl, 63, 64);
+      int base = 0;
+      if (lane == 0 && wtot) base = atomicAdd(s_cur, wtot);
+      base = __shfl(base, 0, 64) + incl - n;
+      const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int song = c * 8 + i;
+        const unsigned v = (ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
+        if (song < bw && v) out[base++] = ((unsigned)song << kCoocCntBits) | v;
+      }
+    }
+  }
+  return make_int2(words, total);
 }
 // range of rows_walk: listener v's entries of tiles [t0, t1)
 struct GroupRange {
@@ -2567,10 +2686,9 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   const int bs = p.block_songs, G = p.grp, ng = p.n_grp;
   const int width = p.song_hi - p.song_lo;
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
-  int* s_scan = reinterpret_cast<int*>(smem_raw + align16(G * bs * 2));
-  int* s_nz = s_scan + 16;                   // [grp] songs first touched per tile
-  int* s_tail = s_nz + kMaxGroupTiles;       // [grp] excess entries per dense tile
-  unsigned short* touched = reinterpret_cast<unsigned short*>(s_tail + kMaxGroupTiles);
+  int* s_tot = reinterpret_cast<int*>(smem_raw + align16(G * bs * 2));  // [grp] non-zeros per tile
+  int* s_cur = s_tot + kMaxGroupTiles;       // [grp] compaction cursors
+  int* s_tail = s_cur + kMaxGroupTiles;      // [grp] excess entries per dense tile
   const int tid = threadIdx.x;
   // big rows (the first n_big): one workgroup per (row, group), a row's groups
   // on one XCD (blocks are dealt round-robin over the 8 XCDs: slot k of XCD x
@@ -2607,37 +2725,26 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     const int lo0 = t0 * bs;  // shard-local first song of the group
     const int gw = min(width, t1 * bs) - lo0;
     for (int i = tid; i < (gw + 1) / 2; i += NT) cnt[i] = 0u;
-    if (tid < kMaxGroupTiles) {
-      s_nz[tid] = 0;
-      s_tail[tid] = 0;
-    }
+    if (tid < 3 * kMaxGroupTiles) s_tot[tid] = 0;  // totals, cursors, excess counters
     __syncthreads();
+    // fire-and-forget adds (no returned value, no per-entry bookkeeping)
     rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs, [&](unsigned key) {
       const unsigned x = key - (unsigned)lo0;
-      const unsigned sh = (x & 1u) << 4;
-      if (((atomicAdd(&cnt[x >> 1], 1u << sh) >> sh) & 0xffffu) == 0u) {
-        const int k = (int)(x / (unsigned)bs);
-        const int j = atomicAdd(&s_nz[k], 1);
-        if (j < kGroupCap) touched[k * kGroupCap + j] = (unsigned short)(x - (unsigned)(k * bs));
-      }
+      atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
     });
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
     for (int k = 0; k < t1 - t0; ++k) {
       const int tile = t0 + k;
       const int bw = min(width, (tile + 1) * bs) - tile * bs;
-      const int total = s_nz[k];
-      const int cb = k * bs;  // tile k's first counter (bs is even: whole words)
       const long long o = big ? p.row_base[r] + (long long)tile * p.tcap : off;
-      const int words = cooc_emit_tile<NT>(p, r, tile, bw, o, total, touched + k * kGroupCap, kGroupCap, s_tail + k,
-                                           s_scan, [&](int i) -> unsigned {
-                                             const int x = cb + i;
-                                             return (cnt[x >> 1] >> ((x & 1) << 4)) & 0xffffu;
-                                           });
-      off += words;
-      row_nz += (unsigned)total;
-      __syncthreads();  // s_scan is rewritten by the next tile; the counters by the next group
+      // tile k's counters start at word k * bs / 2 (bs is a multiple of 256: 16-B aligned)
+      const int2 wt = cooc_emit_tile16<NT>(p, r, tile, bw, o, cnt + (size_t)k * (bs >> 1), s_tot + k, s_cur + k,
+                                           s_tail + k);
+      off += wt.x;
+      row_nz += (unsigned)wt.y;
     }
+    __syncthreads();  // the next group rezeroes the counters
     if (gi == g_begin) stamp_rt(sb, 2);  // the first group's tiles emitted
   }
   if (tid == 0 && row_nz) atomicAdd(&p.row_nnz[r], row_nz);
