@@ -1568,7 +1568,10 @@ constexpr int kWideThreads = 1024;
 #define MR_COOC_U 4         // co-listening route: 16-B pool loads (4 entries) per thread in flight
 #endif
 #ifndef MR_COOC_DU
-#define MR_COOC_DU 4        // co-listening route: dense rows whose 16-B loads are issued together
+#define MR_COOC_DU 4        // co-listening route: dense rows whose loads are issued together
+#endif
+#ifndef MR_COOC_DS
+#define MR_COOC_DS 8        // co-listening route: dense-pass songs per thread per block (8 or 16)
 #endif
 #ifndef MR_COOC_R
 #define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
@@ -1809,41 +1812,42 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       __syncthreads();
       MR_STAMP(12);  // (the last descriptor pass's) descriptors ready
       if (nd > 0) {
-        // 8 songs per thread per block of 8 * NT, every dense row summed in registers
-        for (int b0 = 8 * tid; b0 < bw; b0 += 8 * NT) {
-          unsigned long long a8[8];
+        // DS songs per thread per block of DS * NT, every dense row summed in
+        // registers (DS = 8: one 8-B load per row; 16: one 16-B load per row,
+        // half the blocks per tile)
+        constexpr int DS = MR_COOC_DS;
+        typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
+        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
+          unsigned long long aa[DS];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a8[i] = 0ull;
+          for (int i = 0; i < DS; ++i) aa[i] = 0ull;
           // DU dense rows per step, their loads issued together
           constexpr int DU = MR_COOC_DU;
           for (int d0 = 0; d0 < nd; d0 += DU) {
-            uint2 v0[DU];
+            dvec_t v0[DU];
             unsigned long long qd[DU];
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               const int d = d0 + j;
               qd[j] = 0ull;
-              v0[j] = make_uint2(0u, 0u);
+              v0[j] = dvec_t(0u);
               if (d < nd) {
                 qd[j] = d_q[d];
-                v0[j] = *reinterpret_cast<const uint2*>(p.pool + d_off[d] + (b0 >> 2));
+                v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + d_off[d] + (b0 >> 2));
               }
             }
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
-              unsigned c8[8];
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                c8[i] = (v0[j].x >> (8 * i)) & 0xffu;
-                c8[4 + i] = (v0[j].y >> (8 * i)) & 0xffu;
+              for (int i = 0; i < DS; ++i) {
+                const unsigned c = (v0[j][i >> 2] >> (8 * (i & 3))) & 0xffu;
+                aa[i] += (unsigned long long)c * qd[j];
               }
-#pragma unroll
-              for (int i = 0; i < 8; ++i) a8[i] += (unsigned long long)c8[i] * qd[j];
             }
           }
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
-            if (b0 + i < bw) acc[b0 + i] += a8[i];
+          for (int i = 0; i < DS; ++i)
+            if (b0 + i < bw) acc[b0 + i] += aa[i];
         }
         __syncthreads();  // the sparse walk's atomics may hit any song
       }
@@ -2267,7 +2271,8 @@ __global__ __launch_bounds__(NT, (P16 ? 4 : 2) * NT / 256) void k_cooc_build(Coo
 // ((song + 1) << kLightCntBits) | count slots, open addressing, linear probing,
 // CAS insert; S = mask + 1 slots, hash = the top log2(S) bits of key * φ).
 #ifndef MR_LIGHT_INSERT
-#define MR_LIGHT_INSERT 1  // 1: 4-slot probes (one 16-B LDS read per step); 0: slot by slot;
+#define MR_LIGHT_INSERT 0  // 0: slot by slot; 1: 4-slot probes (one 16-B LDS read per step: slower,
+                           // r04 session 4: C4 8x1 rank 8.29 vs 7.07 ms);
                            // 8, 9: timing-only stubs (wrong counts: no probing / a bare add)
 #endif
 __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int sh, unsigned key) {
@@ -3187,6 +3192,22 @@ int merge_rows_opt() {
 // one XCD, 2 = one tile's users per XCD; MR_WIDE_MAP=1/2 overrides.
 // Light index rows by k_cooc_light (default) or every row per (row, tile)
 // (MR_COOC_LIGHT=0: A/B experiments and tests; read at each mr_load).
+// Largest light-row table (MR_COOC_LIGHT_MAX slots, a power of 2 in
+// [1024, kLightSlots]; rows above it go to the heavy-row kernels) and the
+// table's load bound (MR_COOC_LIGHT_LOAD: entry bound <= this % of the slots,
+// default 80): A/B experiments, read at each mr_load.
+int64_t cooc_light_max_opt() {
+  const char* e = std::getenv("MR_COOC_LIGHT_MAX");
+  int64_t v = e ? std::atoll(e) : kLightSlots;
+  int64_t s = 1024;
+  while (s * 2 <= std::min<int64_t>(v, kLightSlots)) s *= 2;
+  return s;
+}
+int64_t cooc_light_load_opt() {
+  const char* e = std::getenv("MR_COOC_LIGHT_LOAD");
+  const int64_t v = e ? std::atoll(e) : 80;
+  return std::min<int64_t>(100, std::max<int64_t>(10, v));
+}
 bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
   return !(e && std::atoi(e) == 0);
@@ -3786,12 +3807,16 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // light rows (k_cooc_light): the bound fits half the hash slots
       const int64_t nr = (int64_t)row_song.size();
       const bool light_ok = width <= kLightMaxWidth && n_tiles <= kLightMaxTiles && cooc_light_opt();
+      // a light row's table: the smallest power of 2 of at least bound * 100 / lload slots (the
+      // entry bound at most lload % of the slots), at most light_slots_max (MR_COOC_LIGHT_MAX /
+      // MR_COOC_LIGHT_LOAD: A/B knobs; defaults 32768 slots, 80 %)
+      const int64_t lload = cooc_light_load_opt(), light_slots_max = cooc_light_max_opt();
       dense_div = cooc_dense_div_opt();
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
-        if (light_ok && row_base[r] <= light_bound_max(kLightSlots) && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
+        if (light_ok && row_base[r] * 100 <= light_slots_max * lload && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
           int sl = 1024;
-          while (light_bound_max(sl) < row_base[r]) sl <<= 1;
+          while ((int64_t)sl * lload < row_base[r] * 100) sl <<= 1;
           row_slots[r] = sl;
           // lanes per listener of rows_walk: the largest power of 2 G <= 16
           // with 6 G <= the row's shard entries per listener (>= 6 per lane)
