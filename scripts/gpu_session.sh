@@ -96,8 +96,10 @@ esac
 # phase stamps of the wide / co-listening scoring kernel: LSTAMPS="1009318 2000 ibm"
 # build-phase stamps (light rows per tier, heavy-row workgroups): C4 1x1 and the 8x1 shard 0
 case ",$STEPS," in *,bstamps,*)
-  run bstamps_1x1 600 python -u scripts/cooc_build_stamps.py
-  SHARD=0/8 run bstamps_8x1 600 python -u scripts/cooc_build_stamps.py ;;
+  for lib in ${BSTAMPS_LIBS:-stamps}; do
+    MR_ENGINE_LIB=$lib run bstamps_${lib}_1x1 600 python -u scripts/cooc_build_stamps.py
+    SHARD=0/8 MR_ENGINE_LIB=$lib run bstamps_${lib}_8x1 600 python -u scripts/cooc_build_stamps.py
+  done ;;
 esac
 # scoring-kernel phase stamps of the 8x1 shard 0 and of C4 1x1 (co-listening route)
 case ",$STEPS," in *,sstamps,*)
@@ -145,6 +147,13 @@ case ",$STEPS," in *,profs,*)
     for x in "${pairs[@]}"; do [ -n "$x" ] && envs+=("$x"); done
     run prof_$label 600 env "${envs[@]}" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$label" -o p -- python3 "$ROOT/bench.py" --config ${PCFG:-c4} --no-cpu-baseline --no-e2e --no-north-star --steps 3 --warmup 1 --ibm-route cooc
   done ;;
+esac
+# SQ counters of every kernel of the C4 layout probe (one pass, <= 8 SQ counters):
+# LDS-bound vs memory-bound per kernel (reduce with scripts/pmc_summary.py)
+case ",$STEPS," in *,pmcsq,*)
+  export TMPDIR=/tmp
+  MR_PROBE_REPS=1 run pmcsq_a 600 timeout -s KILL 500 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv -d "$OUT/pmcsq_a" -o p -- python3 "$ROOT/scripts/layout_probe.py" ibm ${LAYOUTS:-8x1}
+  MR_PROBE_REPS=1 run pmcsq_b 600 timeout -s KILL 500 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES --kernel-trace --output-format csv -d "$OUT/pmcsq_b" -o p -- python3 "$ROOT/scripts/layout_probe.py" ibm ${LAYOUTS:-8x1} ;;
 esac
 case ",$STEPS," in *,proflayouts,*)
   export TMPDIR=/tmp
