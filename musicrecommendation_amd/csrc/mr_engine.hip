@@ -2333,7 +2333,7 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
 // listener's entries sr_songs[a .. b) (range(v, a, b): the whole shard row
 // for light rows, a tile group's part of it for k_cooc_group; sorted, shard-
 // local ids) in 16-B chunks, lane j the chunks at 4j, 4j + 4G, ..., every
-// entry inserted. G is chosen per row on the host from its entries per
+// entry inserted: ins(k, m) takes a lane's keys of two chunks, k[0 .. m). G is chosen per row on the host from its entries per
 // listener (mr_load: about 6 entries per lane). Software-pipelined: the next
 // listener's row bounds and the id after it are loaded while the current
 // row's first two chunks are inserted. No listener descriptors in LDS, no
@@ -2360,11 +2360,12 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
     c = *reinterpret_cast<const u32x4_a4*>(sr_songs + x);
     return m >= 4 ? 4 : (int)m;
   };
-  auto put = [&](const u32x4_a4& c, int m) {
-    if (m > 0) ins(c.x);
-    if (m > 1) ins(c.y);
-    if (m > 2) ins(c.z);
-    if (m > 3) ins(c.w);
+  // the listener's keys of this iteration as one batch: k[0 .. m) valid (a
+  // chunk's valid entries are a prefix, and the second chunk has entries only
+  // when the first is full, so the two chunks' valid keys are a prefix of 8)
+  auto put2 = [&](const u32x4_a4& c0, int m0, const u32x4_a4& c1, int m1) {
+    const unsigned k[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    ins(k, m0 + m1);
   };
   // iteration i: listeners grp + i * stride + r * step, r < R; the next
   // iteration's row ranges and the one after's ids are loaded while this
@@ -2397,16 +2398,14 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
       v2[r] = l2 < n ? lst[l2] : -1;
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      put(c[r][0], m[r][0]);
-      put(c[r][1], m[r][1]);
-    }
+    for (int r = 0; r < R; ++r) put2(c[r][0], m[r][0], c[r][1], m[r][1]);
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      for (long long x = a0[r] + 4 * j + 8 * G; x < b0[r]; x += 4 * G) {
-        u32x4_a4 cc;
-        const int mm = chunk(x, b0[r], cc);
-        put(cc, mm);
+      for (long long x = a0[r] + 4 * j + 8 * G; x < b0[r]; x += 8 * G) {
+        u32x4_a4 c0, c1;
+        const int m0 = chunk(x, b0[r], c0);
+        const int m1 = chunk(x + 4 * G, b0[r], c1);
+        put2(c0, m0, c1, m1);
       }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -2415,6 +2414,49 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
       v1[r] = v2[r];
     }
   }
+}
+
+// A lane's batch of keys (k[0 .. m), m <= 8) into a light row's table as a
+// queue: each step probes ONE slot for the key at the head, a finished key
+// pops and the next one starts at its home slot the very next step. The wave
+// therefore runs max over lanes of (Σ probes of the lane's keys) steps, not
+// Σ over keys of (max over lanes of its probes), the per-key loop's cost on
+// long linear-probing clusters (C4 8x1: ~30 of a light row's ~40 us walk).
+__device__ __forceinline__ void light_insert_queue(unsigned* tab, unsigned mask, int sh, const unsigned (&k)[8],
+                                                   int m) {
+#if MR_LIGHT_INSERT >= 8
+  for (int i = 0; i < 8; ++i)
+    if (i < m) light_insert(tab, mask, sh, k[i]);
+#else
+  if (m <= 0) return;
+  unsigned q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = k[i];
+  unsigned tag = (q[0] + 1u) << kLightCntBits;
+  unsigned h = (q[0] * 2654435761u) >> sh;
+  int left = m;
+  while (left > 0) {
+    unsigned x = tab[h];
+    bool done = false;
+    if (x == 0u) {
+      x = atomicCAS(&tab[h], 0u, tag | 1u);
+      done = x == 0u;
+    }
+    if (!done && (x & ~kLightCntMask) == tag) {
+      atomicAdd(&tab[h], 1u);
+      done = true;
+    }
+    if (done) {
+      --left;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) q[i] = q[i + 1];
+      tag = (q[0] + 1u) << kLightCntBits;
+      h = (q[0] * 2654435761u) >> sh;
+    } else {
+      h = (h + 1u) & mask;
+    }
+  }
+#endif
 }
 
 // range of rows_walk: listener v's whole shard row
@@ -2457,7 +2499,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   __syncthreads();  // the table and the tile counters are zero
   stamp_rt(sb, 1);
   rows_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
-            [&](unsigned key) { light_insert(tab, mask, sh, key); });
+            [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   __syncthreads();
   stamp_rt(sb, 2);
   // emit: per-tile counts, segment offsets, then the entries
@@ -2536,7 +2578,7 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   wave_lds_sync();  // the table and the tile counters are zero
   stamp_rt_wave(sb, 1);
   rows_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
-            [&](unsigned key) { light_insert(tab, mask, sh, key); });
+            [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
   const int bs = p.block_songs;
@@ -2733,10 +2775,15 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     if (tid < 3 * kMaxGroupTiles) s_tot[tid] = 0;  // totals, cursors, excess counters
     __syncthreads();
     // fire-and-forget adds (no returned value, no per-entry bookkeeping)
-    rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs, [&](unsigned key) {
-      const unsigned x = key - (unsigned)lo0;
-      atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
-    });
+    rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs,
+              [&](const unsigned (&k)[8], int m) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                  if (i < m) {
+                    const unsigned x = k[i] - (unsigned)lo0;
+                    atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
+                  }
+              });
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
     for (int k = 0; k < t1 - t0; ++k) {
