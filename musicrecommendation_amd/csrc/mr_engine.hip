@@ -2055,6 +2055,10 @@ struct CoocParams {
   const unsigned* urec;
   int urec_words, grp, n_grp;
   long long* lstamps;            // diagnostic build: [light row of the launch][8] (k_cooc_light*)
+  // k_cooc_light* / k_cooc_group: the launch's rows as {row, row_slots value,
+  // first listener in trs_users, listeners} (one load instead of rows ->
+  // row_slots / row_song -> trs_off: three dependent ones)
+  const int4* rdesc;
 };
 
 template <bool P16>
@@ -2483,22 +2487,21 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   unsigned* tab = reinterpret_cast<unsigned*>(smem_raw + Lay::tab);
   int* tcnt = reinterpret_cast<int*>(smem_raw + Lay::tcnt);
   int* tpos = reinterpret_cast<int*>(smem_raw + Lay::tpos);
-  const int r = p.rows[blockIdx.x];
+  const int4 rd = p.rdesc[blockIdx.x];  // {row, slots | lane-group log2, listener list start, listeners}
+  const int r = rd.x;
   const int tid = threadIdx.x;
   long long* sb = p.lstamps ? p.lstamps + (size_t)blockIdx.x * 8 : nullptr;
   stamp_rt(sb, 0);
-  const int S = p.row_slots[r] & kLightSlotsMask;
+  const int S = rd.y & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
   for (int i = tid; i < S; i += NT) tab[i] = 0u;
   for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
-  const int s2 = p.row_song[r];
-  const long long la = p.trs_off[s2];
-  const int n = (int)(p.trs_off[s2 + 1] - la);
-  const int* lst = p.trs_users + la;
+  const int n = rd.w;
+  const int* lst = p.trs_users + (unsigned)rd.z;
   __syncthreads();  // the table and the tile counters are zero
   stamp_rt(sb, 1);
-  rows_walk(tid, NT, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+  rows_walk(tid, NT, rd.y >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   __syncthreads();
   stamp_rt(sb, 2);
@@ -2563,21 +2566,20 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   unsigned* tab = reinterpret_cast<unsigned*>(base);
   int* tcnt = reinterpret_cast<int*>(tab + SW);
   int* tpos = tcnt + kWaveMaxTiles;
-  const int r = p.rows[ri];
+  const int4 rd = p.rdesc[ri];
+  const int r = rd.x;
   long long* sb = p.lstamps ? p.lstamps + (size_t)ri * 8 : nullptr;
   stamp_rt_wave(sb, 0);
-  const int S = p.row_slots[r] & kLightSlotsMask;
+  const int S = rd.y & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);
   for (int i = lane; i < S; i += 64) tab[i] = 0u;
   for (int i = lane; i < p.n_tiles; i += 64) { tcnt[i] = 0; tpos[i] = 0; }
-  const int s2 = p.row_song[r];
-  const long long la = p.trs_off[s2];
-  const int n = (int)(p.trs_off[s2 + 1] - la);
-  const int* lst = p.trs_users + la;
+  const int n = rd.w;
+  const int* lst = p.trs_users + (unsigned)rd.z;
   wave_lds_sync();  // the table and the tile counters are zero
   stamp_rt_wave(sb, 1);
-  rows_walk(lane, 64, p.row_slots[r] >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+  rows_walk(lane, 64, rd.y >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
@@ -2644,76 +2646,95 @@ __device__ __forceinline__ int nz_pairs8(const uint4& w, int song0, int bw) {
   return n;
 }
 
-// One tile of a k_cooc_group row written at pool[off] from its u16 counters
-// cw[0 .. bw) (two per word, 16-B aligned): the non-zeros counted from 16-B
-// chunks (8 counters per lane and LDS read, one LDS add per wave), then a dense
-// segment (count bytes + excess entries, as cooc_emit_tile) or a sparse one by
-// compaction — a lane's non-zeros placed at its wave's prefix from a DPP scan,
-// the wave's run reserved by one LDS add per chunk row (order inside the
-// segment unspecified). No per-entry bookkeeping during the walk: the walk's
-// adds are fire-and-forget. s_tot / s_cur / s_tail are zero on entry. Sets
-// seg_off / seg_len; returns (words, non-zeros). Called by the whole workgroup.
+// All tiles [t0, t0 + ntg) of a k_cooc_group pass written from their u16
+// counters (tile k's at cnt + k * bs / 2): pass A counts every tile's
+// non-zeros (16-B LDS chunks, one LDS add per wave and tile), ONE barrier,
+// then every thread derives the same segment offsets — a sparse segment its
+// non-zeros, a dense one its count bytes plus room for as many excess entries
+// as it has non-zeros (an upper bound: within the row's pool bound, see
+// mr_load), so no tile waits for the previous tile's excess count — pass B
+// writes every tile (dense: count bytes + excess entries; sparse: compaction
+// at DPP-scanned wave prefixes, one LDS add per wave and chunk row), ONE
+// barrier, and thread 0 records the segments. s_tot / s_cur / s_tail [ntg]
+// are zero on entry. Advances *off (rows at a running offset) and *row_nz.
 template <int NT>
-__device__ __forceinline__ int2 cooc_emit_tile16(const CoocParams& p, int r, int tile, int bw, long long off,
-                                                 const unsigned* cw, int* s_tot, int* s_cur, int* s_tail) {
+__device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bool big, int t0, int ntg, int bs,
+                                                  int width, const unsigned* cnt, int* s_tot, int* s_cur, int* s_tail,
+                                                  long long* off, unsigned* row_nz) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const int nch = (bw + 7) >> 3;
-  const uint4* cv = reinterpret_cast<const uint4*>(cw);
-  int nz = 0;
-  for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c], c * 8, bw);
-  const int wsum = __shfl(wave_incl_scan(nz), 63, 64);
-  if (lane == 0 && wsum) atomicAdd(s_tot, wsum);
+  for (int k = 0; k < ntg; ++k) {
+    const int bw = min(width, (t0 + k + 1) * bs) - (t0 + k) * bs;
+    const uint4* cv = reinterpret_cast<const uint4*>(cnt + (size_t)k * (bs >> 1));
+    const int nch = (bw + 7) >> 3;
+    int nz = 0;
+    for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c], c * 8, bw);
+    const int ws = __shfl(wave_incl_scan(nz), 63, 64);
+    if (lane == 0 && ws) atomicAdd(&s_tot[k], ws);
+  }
   __syncthreads();
-  const int total = *s_tot;
-  auto count_of = [&](int i) -> unsigned { return (cw[i >> 1] >> ((i & 1) << 4)) & 0xffffu; };
-  unsigned* out = p.pool + off;
-  int words = (total + 3) & ~3;
-  if (p.dense_div > 0 && (long long)total * p.dense_div >= bw) {
+  long long o = *off;
+  for (int k = 0; k < ntg; ++k) {
+    const int tile = t0 + k;
+    const int bw = min(width, (tile + 1) * bs) - tile * bs;
+    const int total = s_tot[k];
+    const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
     const int dwords = cooc_dense_words(bw);
-    for (int i = tid; 4 * i < bw; i += NT) {
-      unsigned wv = 0u;
+    const long long seg = big ? p.row_base[r] + (long long)tile * p.tcap : o;
+    const unsigned* cw = cnt + (size_t)k * (bs >> 1);
+    unsigned* out = p.pool + seg;
+    if (dense) {
+      for (int i = tid; 4 * i < bw; i += NT) {
+        unsigned wv = 0u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = 4 * i + j;
-        const unsigned c = col < bw ? count_of(col) : 0u;
-        wv |= min(c, p.sat) << (8 * j);
-        if (c > p.sat) out[dwords + atomicAdd(s_tail, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
+        for (int j = 0; j < 4; ++j) {
+          const int col = 4 * i + j;
+          const unsigned c = col < bw ? (cw[col >> 1] >> ((col & 1) << 4)) & 0xffffu : 0u;
+          wv |= min(c, p.sat) << (8 * j);
+          if (c > p.sat) out[dwords + atomicAdd(&s_tail[k], 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
+        }
+        out[i] = wv;
       }
-      out[i] = wv;
-    }
-    __syncthreads();
-    const int tail = *s_tail;
-    words = (dwords + tail + 3) & ~3;
-    if (tid == 0) {
-      p.seg_off[(size_t)tile * p.n_rows + r] = off;
-      p.seg_len[(size_t)tile * p.n_rows + r] = kCoocDenseTail - tail;
-    }
-  } else {
-    if (tid == 0) {
-      p.seg_off[(size_t)tile * p.n_rows + r] = off;
-      p.seg_len[(size_t)tile * p.n_rows + r] = total;
-    }
-    for (int c0 = 0; c0 < nch; c0 += NT) {  // wave-uniform trip count (scans inside)
-      const int c = c0 + tid;
-      uint4 w = make_uint4(0u, 0u, 0u, 0u);
-      if (c < nch) w = cv[c];
-      const int n = c < nch ? nz_pairs8(w, c * 8, bw) : 0;
-      const int incl = wave_incl_scan(n);
-      const int wtot = __shfl(incl, 63, 64);
-      int base = 0;
-      if (lane == 0 && wtot) base = atomicAdd(s_cur, wtot);
-      base = __shfl(base, 0, 64) + incl - n;
-      const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+    } else {
+      const uint4* cv = reinterpret_cast<const uint4*>(cw);
+      const int nch = (bw + 7) >> 3;
+      for (int c0 = 0; c0 < nch; c0 += NT) {  // wave-uniform trip count (scans inside)
+        const int c = c0 + tid;
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (c < nch) w = cv[c];
+        const int n = c < nch ? nz_pairs8(w, c * 8, bw) : 0;
+        const int incl = wave_incl_scan(n);
+        const int wtot = __shfl(incl, 63, 64);
+        int base = 0;
+        if (lane == 0 && wtot) base = atomicAdd(&s_cur[k], wtot);
+        base = __shfl(base, 0, 64) + incl - n;
+        const unsigned ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int song = c * 8 + i;
-        const unsigned v = (ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
-        if (song < bw && v) out[base++] = ((unsigned)song << kCoocCntBits) | v;
+        for (int i = 0; i < 8; ++i) {
+          const int song = c * 8 + i;
+          const unsigned v = (ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
+          if (song < bw && v) out[base++] = ((unsigned)song << kCoocCntBits) | v;
+        }
       }
+    }
+    if (!big) o += dense ? ((dwords + total + 3) & ~3) : ((total + 3) & ~3);
+    *row_nz += (unsigned)total;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    long long q = *off;
+    for (int k = 0; k < ntg; ++k) {
+      const int tile = t0 + k;
+      const int bw = min(width, (tile + 1) * bs) - tile * bs;
+      const int total = s_tot[k];
+      const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
+      p.seg_off[(size_t)tile * p.n_rows + r] = big ? p.row_base[r] + (long long)tile * p.tcap : q;
+      p.seg_len[(size_t)tile * p.n_rows + r] = dense ? kCoocDenseTail - s_tail[k] : total;
+      if (!big) q += dense ? ((cooc_dense_words(bw) + total + 3) & ~3) : ((total + 3) & ~3);
     }
   }
-  return make_int2(words, total);
+  *off = o;
 }
+
 // range of rows_walk: listener v's entries of tiles [t0, t1)
 struct GroupRange {
   const unsigned* rec;
@@ -2757,12 +2778,11 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     g_begin = 0;
     g_end = ng;
   }
-  const int r = p.rows[ri];
-  const int s2 = p.row_song[r];
-  const long long la = p.trs_off[s2];
-  const int n = (int)(p.trs_off[s2 + 1] - la);
-  const int* lst = p.trs_users + la;
-  const int glog = p.row_slots[r] >> kLightGlogShift;
+  const int4 rd = p.rdesc[ri];
+  const int r = rd.x;
+  const int n = rd.w;
+  const int* lst = p.trs_users + (unsigned)rd.z;
+  const int glog = rd.y >> kLightGlogShift;
   long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
   stamp_rt(sb, 0);
   long long off = p.row_base[r];
@@ -2786,17 +2806,11 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
               });
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
-    for (int k = 0; k < t1 - t0; ++k) {
-      const int tile = t0 + k;
-      const int bw = min(width, (tile + 1) * bs) - tile * bs;
-      const long long o = big ? p.row_base[r] + (long long)tile * p.tcap : off;
-      // tile k's counters start at word k * bs / 2 (bs is a multiple of 256: 16-B aligned)
-      const int2 wt = cooc_emit_tile16<NT>(p, r, tile, bw, o, cnt + (size_t)k * (bs >> 1), s_tot + k, s_cur + k,
-                                           s_tail + k);
-      off += wt.x;
-      row_nz += (unsigned)wt.y;
-    }
-    __syncthreads();  // the next group rezeroes the counters
+    // tile k's counters start at word k * bs / 2 (bs is a multiple of 256: 16-B aligned)
+    cooc_emit_group16<NT>(p, r, big, t0, t1 - t0, bs, width, cnt, s_tot, s_cur, s_tail, &off, &row_nz);
+    // thread 0 reads s_tot / s_tail after the emission's closing barrier: keep
+    // the next group's zeroing behind it (the dc4df36 race class)
+    __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 2);  // the first group's tiles emitted
   }
   if (tid == 0 && row_nz) atomicAdd(&p.row_nnz[r], row_nz);
@@ -3130,6 +3144,7 @@ struct mr_ctx {
   size_t bstamp_off = 0;           // diagnostic build: k_cooc_build's stamps in the stamps buffer
   size_t lstamp_off = 0;           //   and the light rows' (one slot block per light row, launch order)
   DevBuf<int> rows_order, row_slots;  // heavy rows then light rows; light rows' hash slots
+  DevBuf<int4> rdesc;              // rows_order's rows as {row, row_slots, listener start, listeners}
   DevBuf<long long> sr_off;        // light rows / k_cooc_group: the shard's train rows
   DevBuf<unsigned> sr_songs;
   DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts
@@ -3149,7 +3164,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    urec.release(); grp = n_grp = urec_words = 0;
+    urec.release(); rdesc.release(); grp = n_grp = urec_words = 0;
     row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -4009,6 +4024,15 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
+    {
+      std::vector<int4> rd(std::max<size_t>(1, order.size()));
+      for (size_t i = 0; i < order.size(); ++i) {
+        const int32_t r = order[i], s2 = row_song[r];
+        rd[i] = make_int4(r, row_slots[r], (int)trs_off[s2], (int)(trs_off[s2 + 1] - trs_off[s2]));
+      }
+      if ((rc = dev_upload(c->rdesc, rd.data(), rd.size(), st))) return rc;
+      MR_HIP(hipStreamSynchronize(st));
+    }
     if ((rc = dev_upload(c->row_slots, row_slots.data(), row_slots.size(), st))) return rc;
     if (!light_rows.empty() || grp > 0) {
       // the shard's train rows, shard-local song ids (k_cooc_light's and
@@ -4351,6 +4375,7 @@ int run_cooc(mr_ctx* c) {
       hp.urec_words = c->urec_words;
       hp.grp = c->grp;
       hp.n_grp = c->n_grp;
+      hp.rdesc = c->rdesc.p + n32;
       if (hp.stamps) hp.stamps += (size_t)n32 * c->n_tiles * 8;
       const int nblk = (c->n_big16 + 7) / 8 * 8 * c->n_grp + (n16 - c->n_big16);
       const size_t glds = (size_t)cooc_group_lds(c->block_songs, c->grp);
@@ -4378,6 +4403,7 @@ int run_cooc(mr_ctx* c) {
       if (c->n_light_tier[t] == 0) continue;
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + lr;
+      lp.rdesc = c->rdesc.p + lr;
       lp.lstamps = c->stamps.p ? c->stamps.p + c->lstamp_off + (size_t)(lr - c->n_heavy) * 8 : nullptr;
       hipStream_t ls = side ? c->side[t < 2 ? 0 : 1] : st;
       if (int rc2 = light_tier_call(t, ls, c->n_light_tier[t], &lp, lp)) return rc2;
