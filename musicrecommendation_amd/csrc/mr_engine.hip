@@ -1573,6 +1573,10 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_DS
 #define MR_COOC_DS 8        // co-listening route: dense-pass songs per thread per block (8 or 16)
 #endif
+#ifndef MR_COOC_PF
+#define MR_COOC_PF 0        // co-listening scoring: per-song scales prefetched per thread (songs tid + NT e;
+                            // 0 = none)
+#endif
 #ifndef MR_COOC_R
 #define MR_COOC_R 2         // co-listening index build: listeners per thread per iteration
 #endif
@@ -1739,6 +1743,20 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   const int bw = bhi - blo;
   MR_STAMP(0);
 
+  // co-listening route: the epilogue's per-song scales of this thread's songs
+  // (i = tid + NT e) loaded now, in flight while stage 2 runs (a tile's
+  // scales are the same for every user: L2 hits, but three dependent batches
+  // of them were ~2 us of the epilogue)
+  constexpr bool kPF = COOC && MR_COOC_PF > 0;
+  constexpr int PF = kPF ? MR_COOC_PF : 1;
+  double scp[PF];
+  if constexpr (kPF) {
+#pragma unroll
+    for (int e = 0; e < PF; ++e) {
+      const int i = tid + e * NT;
+      scp[e] = i < bw ? p.sqrt_c[blo + i] : 1.0;
+    }
+  }
   for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += NT) heard[i] = 0u;
   __syncthreads();
@@ -1933,7 +1951,23 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   long long mk = kKeyNone;
   int ms = INT_MAX;
   constexpr int EB = MR_WIDE_EB;
-  for (int i0 = tid; i0 < bw; i0 += EB * NT) {
+  int i_start = tid;
+  if constexpr (kPF) {  // the prefetched songs first
+#pragma unroll
+    for (int e = 0; e < PF; ++e) {
+      const int i = tid + e * NT;
+      if (i >= bw) continue;
+      const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
+      double score = (double)(long long)acc[i] * inv_f;
+      score = score / scp[e];
+      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      const long long key = h ? kKeyNone : __double_as_longlong(score);
+      acc[i] = (unsigned long long)key;
+      if (key >= 0) take_if_before(mk, ms, key, blo + i);
+    }
+    i_start = tid + PF * NT;
+  }
+  for (int i0 = i_start; i0 < bw; i0 += EB * NT) {
     double sc[EB];
     unsigned long long av[EB];
 #pragma unroll
