@@ -3292,9 +3292,14 @@ int merge_rows_opt() {
 // [1024, kLightSlots]; rows above it go to the heavy-row kernels) and the
 // table's load bound (MR_COOC_LIGHT_LOAD: entry bound <= this % of the slots,
 // default 80): A/B experiments, read at each mr_load.
-int64_t cooc_light_max_opt() {
+// Default: the largest table (kLightSlots) — unless the shard is narrow enough
+// for k_cooc_group to hold ALL its tiles in one pass (C4 over 8 GPUs: 3 tiles
+// of 15.6k songs): then one listener walk with fire-and-forget counter adds
+// beats hashing for the larger rows, and light rows stop at kLightSlotsNarrow.
+constexpr int64_t kLightSlotsNarrow = 16384;
+int64_t cooc_light_max_opt(bool narrow) {
   const char* e = std::getenv("MR_COOC_LIGHT_MAX");
-  int64_t v = e ? std::atoll(e) : kLightSlots;
+  int64_t v = e ? std::atoll(e) : (narrow ? kLightSlotsNarrow : kLightSlots);
   int64_t s = 1024;
   while (s * 2 <= std::min<int64_t>(v, kLightSlots)) s *= 2;
   return s;
@@ -3906,7 +3911,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // a light row's table: the smallest power of 2 of at least bound * 100 / lload slots (the
       // entry bound at most lload % of the slots), at most light_slots_max (MR_COOC_LIGHT_MAX /
       // MR_COOC_LIGHT_LOAD: A/B knobs; defaults 32768 slots, 80 %)
-      const int64_t lload = cooc_light_load_opt(), light_slots_max = cooc_light_max_opt();
+      // narrow shard: the group kernel would hold every tile in one pass
+      // (the conditions of its set-up below, before the heavy rows are known)
+      bool narrow = false;
+      if (cooc_group_opt() && 1 + (n_tiles + 2) / 2 <= 32 && max_shard_deg <= 65535 &&
+          n_tiles <= std::min(kMaxGroupTiles, cooc_group_max_opt()))
+        narrow = cooc_group_lds(bs, n_tiles) <= kLdsBytes;
+      const int64_t lload = cooc_light_load_opt(), light_slots_max = cooc_light_max_opt(narrow);
       dense_div = cooc_dense_div_opt();
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {

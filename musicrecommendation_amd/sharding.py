@@ -6,7 +6,10 @@ layout inside the C ABI for single-process callers):
 
 * song-range shards (the north star; the reference's Spark "strategy 2",
   distributed.scala:477-479 ``parallelize(songs, 4)``): every rank holds the
-  whole train CSR (stage 1 is replicated) and scores songs [lo, hi). Dense
+  whole train CSR and scores songs [lo, hi). On the ItemBasedModel's
+  co-listening route nothing is replicated: each rank builds
+  the index columns of its own songs only (on the two-hop route, stage 1 —
+  the neighbour weights — is recomputed by every shard of a user block). Dense
   rows stay sharded by column; the per-test-user top-k lists travel as one
   record block per rank (int64 keys, then int32 songs) exchanged with ONE
   all-gather and merged by (key desc, song asc). Fixed-point keys make the merge order-independent,
