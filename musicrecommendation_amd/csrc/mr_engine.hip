@@ -1573,6 +1573,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_DS
 #define MR_COOC_DS 8        // co-listening route: dense-pass songs per thread per block (8 or 16)
 #endif
+#ifndef MR_GROUP_STUB
+#define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
+#endif
 #ifndef MR_COOC_PF
 #define MR_COOC_PF 0        // co-listening scoring: per-song scales prefetched per thread (songs tid + NT e;
                             // 0 = none)
@@ -2712,6 +2715,11 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     const int bw = min(width, (tile + 1) * bs) - tile * bs;
     const int total = s_tot[k];
     const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
+#if MR_GROUP_STUB == 2  // timing-only build: pass A only
+    if (!big) o += dense ? ((cooc_dense_words(bw) + total + 3) & ~3) : ((total + 3) & ~3);
+    *row_nz += (unsigned)total;
+    continue;
+#endif
     const int dwords = cooc_dense_words(bw);
     const long long seg = big ? p.row_base[r] + (long long)tile * p.tcap : o;
     const unsigned* cw = cnt + (size_t)k * (bs >> 1);
@@ -2742,12 +2750,16 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
         if (lane == 0 && wtot) base = atomicAdd(&s_cur[k], wtot);
         base = __shfl(base, 0, 64) + incl - n;
         const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#if MR_GROUP_STUB != 1  // (1: timing-only build without the sparse stores)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int song = c * 8 + i;
           const unsigned v = (ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
           if (song < bw && v) out[base++] = ((unsigned)song << kCoocCntBits) | v;
         }
+#else
+        if (base < 0) out[0] = ww[0];
+#endif
       }
     }
     if (!big) o += dense ? ((dwords + total + 3) & ~3) : ((total + 3) & ~3);
