@@ -2673,14 +2673,16 @@ __host__ __device__ inline int cooc_group_lds(int bs, int g) {
   return align16(g * bs * 2) + 3 * kMaxGroupTiles * 4;  // counters; per tile: total, cursor, excess
 }
 
-// Non-zero u16 counters among the 8 of a 16-B chunk (songs song0 .. song0 + 7
-// of a tile of bw songs).
-__device__ __forceinline__ int nz_pairs8(const uint4& w, int song0, int bw) {
-  int n = 0;
-  const unsigned ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) n += (song0 + i < bw && ((ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu)) ? 1 : 0;
-  return n;
+// Bit 15 / bit 31 of the result set iff the low / high u16 half of x is non-zero
+// (the low 15 bits + 0x7fff carry into bit 15; OR-ing x catches bit 15 itself).
+__device__ __forceinline__ unsigned nz_halves(unsigned x) {
+  return (((x & 0x7fff7fffu) + 0x7fff7fffu) | x) & 0x80008000u;
+}
+// Non-zero u16 counters among the 8 of a 16-B chunk. k_cooc_group zeroes the
+// counters up to the last chunk's end, so a tile's padding past its bw songs
+// counts nothing.
+__device__ __forceinline__ int nz_pairs8(const uint4& w) {
+  return __popc(nz_halves(w.x) | (nz_halves(w.y) >> 1) | (nz_halves(w.z) >> 2) | (nz_halves(w.w) >> 3));
 }
 
 // All tiles [t0, t0 + ntg) of a k_cooc_group pass written from their u16
@@ -2704,7 +2706,7 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     const uint4* cv = reinterpret_cast<const uint4*>(cnt + (size_t)k * (bs >> 1));
     const int nch = (bw + 7) >> 3;
     int nz = 0;
-    for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c], c * 8, bw);
+    for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c]);
     const int ws = __shfl(wave_incl_scan(nz), 63, 64);
     if (lane == 0 && ws) atomicAdd(&s_tot[k], ws);
   }
@@ -2743,19 +2745,19 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
         const int c = c0 + tid;
         uint4 w = make_uint4(0u, 0u, 0u, 0u);
         if (c < nch) w = cv[c];
-        const int n = c < nch ? nz_pairs8(w, c * 8, bw) : 0;
+        const int n = nz_pairs8(w);  // (w is zero past the tile)
         const int incl = wave_incl_scan(n);
         const int wtot = __shfl(incl, 63, 64);
         int base = 0;
         if (lane == 0 && wtot) base = atomicAdd(&s_cur[k], wtot);
-        base = __shfl(base, 0, 64) + incl - n;
+        unsigned pos = (unsigned)(__shfl(base, 0, 64) + incl - n);
         const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+        const unsigned key0 = (unsigned)(c * 8) << kCoocCntBits;
 #if MR_GROUP_STUB != 1  // (1: timing-only build without the sparse stores)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int song = c * 8 + i;
           const unsigned v = (ww[i >> 1] >> ((i & 1) << 4)) & 0xffffu;
-          if (song < bw && v) out[base++] = ((unsigned)song << kCoocCntBits) | v;
+          if (v) out[pos++] = (key0 | ((unsigned)i << kCoocCntBits)) | v;
         }
 #else
         if (base < 0) out[0] = ww[0];
@@ -2793,6 +2795,137 @@ struct GroupRange {
     b = base + st[t1];
   }
 };
+
+// A k_cooc_group pass's counters zeroed up to the last 16-B chunk's end (the
+// emission's chunk counts need no bound test), and its per-tile totals,
+// cursors and excess counters.
+template <int NT>
+__device__ __forceinline__ void group_zero(unsigned* cnt, int gw, int* s_tot) {
+  uint4* c4 = reinterpret_cast<uint4*>(cnt);
+  for (int i = threadIdx.x; i < (gw + 7) >> 3; i += NT) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (threadIdx.x < 3 * kMaxGroupTiles) s_tot[threadIdx.x] = 0;
+}
+
+// Entries x .. x + 3 of sr_songs below b (a prefix of the chunk) or none.
+__device__ __forceinline__ int group_chunk(const unsigned* songs, unsigned x, unsigned b, u32x4_a4& c) {
+  c = u32x4_a4{0u, 0u, 0u, 0u};
+  if (x >= b) return 0;
+  c = *reinterpret_cast<const u32x4_a4*>(songs + x);
+  const unsigned m = b - x;
+  return m >= 4u ? 4 : (int)m;
+}
+
+// A chunk's m valid songs counted (u16 pairs: song x's counter is the half
+// x & 1 of word x >> 1; fire-and-forget LDS adds).
+__device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int m, unsigned lo0) {
+  const unsigned k[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < m) {
+      const unsigned x = k[i] - lo0;
+      atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
+    }
+}
+
+// k_cooc_group's rows under kCoocBigRow listeners, every tile group in turn
+// with the walk software-pipelined ACROSS groups: each lane group holds up to
+// kGroupPipeR listeners for the whole row (mr_load caps the lanes per listener
+// so that the row fits: n <= (NT >> glog) * kGroupPipeR), their ids and record
+// bases are loaded once, the next group's end is loaded while this group is
+// walked, and the next group's first two chunks per listener are issued before
+// this group's emission, so they land while the tiles are written. The
+// per-group walk of rows_walk repeated the whole dependent chain (listener id
+// -> record -> chunk, ~3 x 3-5 us under load) for every group: C4 1x1 15.4 us
+// of a group pass's ~32 (profiles/r04/s9).
+#ifndef MR_GROUP_PIPE
+#define MR_GROUP_PIPE 1
+#endif
+constexpr int kGroupPipeR = 4;
+template <int NT>
+__device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const int* lst, int n, int glog,
+                                                     int width, unsigned* cnt, int* s_tot, int* s_cur, int* s_tail,
+                                                     long long* sb, long long* off, unsigned* row_nz) {
+  constexpr int R = kGroupPipeR;
+  const int tid = threadIdx.x;
+  const int L = 1 << glog, j = tid & (L - 1), lg = tid >> glog, step = NT >> glog;
+  const int bs = p.block_songs, GT = p.grp, nt = p.n_tiles, ng = p.n_grp, words = p.urec_words;
+  const unsigned* songs = p.sr_songs;
+  // listener i of this lane group: lg + i * step; its entries of the current
+  // group: [a, b) of sr_songs (records hold 32-bit bases, mr_load)
+  int v[R];
+  unsigned base[R], a[R], b[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int l = lg + i * step;
+    v[i] = l < n ? lst[l] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    base[i] = a[i] = b[i] = 0u;
+    if (v[i] >= 0) {
+      const unsigned* q = p.urec + (size_t)v[i] * words;
+      const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
+      base[i] = q[0];
+      a[i] = base[i] + st[0];
+      b[i] = base[i] + st[min(nt, GT)];
+    }
+  }
+  u32x4_a4 c[R][2];
+  int m[R][2];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const unsigned x = a[i] + 4u * j;
+    m[i][0] = group_chunk(songs, x, b[i], c[i][0]);
+    m[i][1] = group_chunk(songs, x + 4u * L, b[i], c[i][1]);
+  }
+  for (int gi = 0; gi < ng; ++gi) {
+    const int t0 = gi * GT, t1 = min(nt, t0 + GT), t2 = min(nt, t1 + GT);
+    const unsigned lo0 = (unsigned)(t0 * bs);  // shard-local first song of the group
+    const int gw = min(width, t1 * bs) - t0 * bs;
+    group_zero<NT>(cnt, gw, s_tot);
+    // the next group's end (its start is this group's end)
+    unsigned e[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      e[i] = b[i];
+      if (v[i] >= 0 && gi + 1 < ng)
+        e[i] = base[i] + reinterpret_cast<const unsigned short*>(p.urec + (size_t)v[i] * words + 1)[t2];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      group_add(cnt, c[i][0], m[i][0], lo0);
+      group_add(cnt, c[i][1], m[i][1], lo0);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      for (unsigned x = a[i] + 4u * j + 8u * L; x < b[i]; x += 8u * L) {
+        u32x4_a4 d0, d1;
+        const int m0 = group_chunk(songs, x, b[i], d0);
+        const int m1 = group_chunk(songs, x + 4u * L, b[i], d1);
+        group_add(cnt, d0, m0, lo0);
+        group_add(cnt, d1, m1, lo0);
+      }
+    __syncthreads();
+    if (gi == 0) stamp_rt(sb, 1);  // the first group's walk done
+    // the next group's first chunks: in flight while this group is emitted
+    if (gi + 1 < ng) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        a[i] = b[i];
+        b[i] = e[i];
+        const unsigned x = a[i] + 4u * j;
+        m[i][0] = group_chunk(songs, x, b[i], c[i][0]);
+        m[i][1] = group_chunk(songs, x + 4u * L, b[i], c[i][1]);
+      }
+    }
+    cooc_emit_group16<NT>(p, r, false, t0, t1 - t0, bs, width, cnt, s_tot, s_cur, s_tail, off, row_nz);
+    // thread 0 reads s_tot / s_tail after the emission's closing barrier: keep
+    // the next group's zeroing behind it
+    __syncthreads();
+    if (gi == 0) stamp_rt(sb, 2);  // the first group's tiles emitted
+  }
+}
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
@@ -2833,12 +2966,17 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   stamp_rt(sb, 0);
   long long off = p.row_base[r];
   unsigned row_nz = 0u;
+#if MR_GROUP_PIPE
+  if (!big && n <= (NT >> glog) * kGroupPipeR) {
+    cooc_group_pipelined<NT>(p, r, lst, n, glog, width, cnt, s_tot, s_cur, s_tail, sb, &off, &row_nz);
+    g_end = g_begin;  // (every group done)
+  }
+#endif
   for (int gi = g_begin; gi < g_end; ++gi) {
     const int t0 = gi * G, t1 = min(p.n_tiles, t0 + G);
     const int lo0 = t0 * bs;  // shard-local first song of the group
     const int gw = min(width, t1 * bs) - lo0;
-    for (int i = tid; i < (gw + 1) / 2; i += NT) cnt[i] = 0u;
-    if (tid < 3 * kMaxGroupTiles) s_tot[tid] = 0;  // totals, cursors, excess counters
+    group_zero<NT>(cnt, gw, s_tot);
     __syncthreads();
     // fire-and-forget adds (no returned value, no per-entry bookkeeping)
     rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs,
@@ -2863,7 +3001,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   stamp_rt(sb, 4);
   stamp_val(sb, 5, big ? 1 : 0);
   stamp_val(sb, 6, n);
-  stamp_val(sb, 7, g_end - g_begin);
+  stamp_val(sb, 7, big ? 1 : p.n_grp);
 }
 
 // The records of k_cooc_group, built once per load: one thread per train user
@@ -4000,6 +4138,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           const int64_t per = cr > 0 ? (row_reads[r] - cr) / cr * grp / n_tiles : 0;
           int glog = 0;
           while (glog < 4 && ((int64_t)6 << (glog + 1)) <= per) ++glog;
+          // rows under kCoocBigRow listeners: every listener held by a lane
+          // group for the whole row (cooc_group_pipelined)
+          if ((int)i >= n_heavy32 + n_big16)
+            while (glog > 0 && cr > (int64_t)(cooc_group_nt_opt() >> glog) * kGroupPipeR) --glog;
           row_slots[r] = glog << kLightGlogShift;
         }
       } else {
