@@ -132,7 +132,15 @@ case ",$STEPS," in *,probes,*)
     envs=()
     IFS=',' read -ra pairs <<< "$kv"
     for x in "${pairs[@]}"; do [ -n "$x" ] && envs+=("$x"); done
-    run probe_$label 600 env "${envs[@]}" MR_PROBE_REPS=${REPS:-3} python -u scripts/layout_probe.py ibm ${LAYOUTS:-1x1,8x1}
+    run probe_$label 600 env "${envs[@]}" MR_PROBE_REPS=${REPS:-3} python -u scripts/layout_probe.py ${PMODELS:-ibm} ${LAYOUTS:-1x1,8x1}
+  done ;;
+esac
+# C5's two dense models per rank of each layout (C5LAYOUTS), then the ubm model at
+# 1x1 under each wide block mapping (C5MAPS="1 2 3", MR_WIDE_MAP)
+case ",$STEPS," in *,c5probe,*)
+  MR_PROBE_CONFIG=c5 MR_PROBE_DENSE=1 MR_PROBE_REPS=${REPS:-2} run c5_layouts 900 python -u scripts/layout_probe.py ubm,ibm ${C5LAYOUTS:-1x1,8x1,2x4}
+  for m in ${C5MAPS:-}; do
+    MR_WIDE_MAP=$m MR_PROBE_CONFIG=c5 MR_PROBE_DENSE=1 MR_PROBE_REPS=${REPS:-2} run c5_map$m 600 python -u scripts/layout_probe.py ubm 1x1
   done ;;
 esac
 # rocprofv3 kernel stats of C4 (1x1, co-listening route, 3 steps) under engine-option
