@@ -1035,10 +1035,6 @@ struct ScoreParams {
   const long long* seg_off;      // [tile][row]: first pool entry of the row's tile segment
   const int* seg_len;            // [tile][row]: its entries
   const unsigned* pool;          // entries (tile-local song << kCoocCntBits) | C[s2][s]
-  // wide two-hop walk over per-user records (walk_user_lists; null: toff / tsongs)
-  const unsigned* urec;          // [n_tr][urec_words]: shard-row base, then u16 tile starts
-  int urec_words;
-  const unsigned* sr_songs;      // user-major shard rows, shard-local song ids
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -1708,70 +1704,6 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
   (void)v0;
 }
 
-// walk_tile_lists over v-major data: list entry v's songs of this tile are
-// sr_songs[base + st[tile] .. base + st[tile + 1]) (urec: v's shard-row base
-// and u16 tile starts in one line; sr_songs: its shard row, shard-local ids,
-// padded by 4 entries so a 16-B chunk load never leaves the buffer). Every
-// tile of a user reads the SAME record line and shard-row lines of each
-// neighbour (tile-major toff / tsongs: a different line pair per tile), so
-// with a user's tiles on one XCD (xcd_remap 1) the other tiles find them in
-// L2. Same three-level software pipeline; the first kSeg entries as 16-B
-// chunks, longer segments loop.
-template <int NT, int R, int kSeg, typename WT, typename LoadList, typename Add>
-__device__ __forceinline__ void walk_user_lists(int tid, int cnt, LoadList&& load_list, const unsigned* urec, int words,
-                                                int tile, unsigned lo, const unsigned* songs, Add&& add) {
-  auto load_offs = [&](const int (&v)[R], unsigned (&a)[R], unsigned (&b)[R]) {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      a[r] = b[r] = 0u;
-      if (v[r] >= 0) {
-        const unsigned* q = urec + (size_t)v[r] * words;
-        const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
-        const unsigned base = q[0];
-        a[r] = base + st[tile];
-        b[r] = base + st[tile + 1];
-      }
-    }
-  };
-  constexpr int kC = (kSeg + 3) / 4;
-  int v0[R], v1[R], v2[R];
-  unsigned a0[R], b0[R], a1[R], b1[R];
-  WT q0[R], q1[R], q2[R];
-  load_list(tid, v0, q0);
-  load_offs(v0, a0, b0);
-  load_list(tid + R * NT, v1, q1);
-  for (int k0 = tid; k0 < cnt; k0 += R * NT) {
-    u32x4_a4 sw[R][kC];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int j = 0; j < kC; ++j) {
-        const unsigned x = a0[r] + 4u * j;
-        sw[r][j] = x < b0[r] ? *reinterpret_cast<const u32x4_a4*>(songs + x) : u32x4_a4{0u, 0u, 0u, 0u};
-      }
-    load_offs(v1, a1, b1);                 // iteration i+1
-    load_list(k0 + 2 * R * NT, v2, q2);    // iteration i+2
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-#pragma unroll
-      for (int j = 0; j < 4 * kC; ++j)
-        if (a0[r] + j < b0[r]) add(sw[r][j >> 2][j & 3] - lo, q0[r]);
-      for (unsigned x0 = a0[r] + 4u * kC; x0 < b0[r]; x0 += 4u) {
-        const u32x4_a4 c = *reinterpret_cast<const u32x4_a4*>(songs + x0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (x0 + j < b0[r]) add(c[j] - lo, q0[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      a0[r] = a1[r]; b0[r] = b1[r]; q0[r] = q1[r];
-      v1[r] = v2[r]; q1[r] = q2[r];
-    }
-  }
-  (void)v0;
-}
-
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
 template <int MODEL, typename OutT, int NT, int KS, bool COOC>
@@ -2007,13 +1939,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         }
       }
     };
-    if (p.urec)
-      walk_user_lists<NT, R, kSeg, unsigned long long>(tid, cnt, load_list, p.urec, p.urec_words, tile,
-                                                       (unsigned)(tile * bs), p.sr_songs,
-                                                       [&](unsigned x, unsigned long long q) { atomicAdd(&acc[x], q); });
-    else
-      walk_tile_lists<NT, R, kSeg, unsigned long long>(tid, cnt, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
-                                                       [&](unsigned x, unsigned long long q) { atomicAdd(&acc[x], q); });
+    walk_tile_lists<NT, R, kSeg, unsigned long long>(tid, cnt, load_list, p.toff + (size_t)tile * p.n_tr, p.tsongs,
+                                                     [&](unsigned x, unsigned long long q) { atomicAdd(&acc[x], q); });
   }
   __syncthreads();
   MR_STAMP(2);
@@ -3406,7 +3333,6 @@ struct mr_ctx {
   DevBuf<unsigned> sr_songs;
   DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts
   int grp = 0, n_grp = 0, urec_words = 0;
-  bool vrec = false;               // two-hop wide walks over urec / sr_songs (walk_user_lists)
   int group_nt = 1024;             // threads per k_cooc_group workgroup (MR_COOC_GNT)
 
   void release_data() {
@@ -3422,7 +3348,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    urec.release(); rdesc.release(); grp = n_grp = urec_words = 0; vrec = false;
+    urec.release(); rdesc.release(); grp = n_grp = urec_words = 0;
     row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -3555,12 +3481,6 @@ int cooc_nt_opt() {
 int cooc_group_nt_opt() {
   const char* e = std::getenv("MR_COOC_GNT");
   return e && std::atoi(e) == 512 ? 512 : 1024;
-}
-// The two-hop wide walk over per-user records and shard rows (walk_user_lists;
-// default) or over the tile-major toff / tsongs (MR_WIDE_VREC=0: A/B, tests).
-bool wide_vrec_opt() {
-  const char* e = std::getenv("MR_WIDE_VREC");
-  return !(e && std::atoi(e) == 0);
 }
 int cooc_group_max_opt() {
   const char* e = std::getenv("MR_COOC_GRP");
@@ -4313,33 +4233,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       MR_HIP(hipStreamSynchronize(st));
     }
     if ((rc = dev_upload(c->row_slots, row_slots.data(), row_slots.size(), st))) return rc;
-  }
-  // The ubm wide walk over per-user records (walk_user_lists): every tile's
-  // start of a user in one u16 record line (n_tiles <= 60, shard rows < 65536)
-  bool vrec = false;
-  if (wide && !fused && wide_vrec_opt() && n_tiles <= 60 && n_tr > 0) {
-    int32_t md = max_shard_deg;
-    if (route != 2) {
-      std::vector<int32_t> dg((size_t)n_tr);
-      mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
-        for (int64_t v = a; v < b; ++v) {
-          const int32_t* r0 = tr_songs + tr_off[v];
-          const int32_t* r1 = tr_songs + tr_off[v + 1];
-          dg[v] = (int32_t)(std::lower_bound(r0, r1, hi) - std::lower_bound(r0, r1, lo));
-        }
-      });
-      md = *std::max_element(dg.begin(), dg.end());
-    }
-    vrec = md <= 65535;
-    if (vrec && grp == 0) {
-      urec_words = 1;
-      while (urec_words < 1 + (n_tiles + 2) / 2) urec_words <<= 1;
-    }
-  }
-  {
-    if ((route == 2 && (!light_rows.empty() || grp > 0)) || vrec) {
-      // the shard's train rows, shard-local song ids (k_cooc_light's,
-      // k_cooc_group's and walk_user_lists' input)
+    if (!light_rows.empty() || grp > 0) {
+      // the shard's train rows, shard-local song ids (k_cooc_light's and
+      // k_cooc_group's input)
       std::vector<int64_t> so((size_t)n_tr + 1, 0);
       mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
         for (int64_t v = a; v < b; ++v) {
@@ -4360,7 +4256,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       });
       if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
       if ((rc = dev_upload(c->sr_songs, ss.data(), ss.size(), st))) return rc;
-      if (grp > 0 || vrec) {  // per-user records (tile starts), on the device
+      if (grp > 0) {  // k_cooc_group's per-user records (tile starts), on the device
         if ((rc = dev_alloc(c->urec, (size_t)std::max(1, n_tr) * urec_words))) return rc;
         hipLaunchKernelGGL(k_urec, dim3((std::max(1, n_tr) + 255) / 256), dim3(256), 0, st, c->sr_off.p,
                            c->sr_songs.p, n_tr, n_tiles, bs, urec_words, c->urec.p);
@@ -4410,8 +4306,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     MR_HIP(hipFuncSetAttribute((const void*)c->nbr_kernel[m], hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)c->nbr_lds));
   }
-  c->urec_words = urec_words;
-  c->vrec = vrec;
   if (route == 2) {
     c->n_rows = (int)row_song.size();
     c->pool_cap = pool_cap;
@@ -4437,6 +4331,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->n_big16 = n_big16;
     c->grp = grp;
     c->n_grp = n_grp;
+    c->urec_words = urec_words;
     c->group_nt = cooc_group_nt_opt();
     if (grp > 0)
       MR_HIP(hipFuncSetAttribute(c->group_nt == 512 ? (const void*)k_cooc_group<512> : (const void*)k_cooc_group<1024>,
@@ -4827,11 +4722,6 @@ int run_model(mr_ctx* c, int model) {
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       sp.topk_lists = c->opt.topk_lists;
-      if (wide && c->vrec) {
-        sp.urec = c->urec.p;
-        sp.urec_words = c->urec_words;
-        sp.sr_songs = c->sr_songs.p;
-      }
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
                          c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
