@@ -1576,9 +1576,6 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
-#ifndef MR_COOC_DOT
-#define MR_COOC_DOT 1       // co-listening scoring: dense rows by u16-limb dot products (0: u64 multiply-adds)
-#endif
 #ifndef MR_COOC_PF
 #define MR_COOC_PF 0        // co-listening scoring: per-song scales prefetched per thread (songs tid + NT e;
                             // 0 = none)
@@ -1841,80 +1838,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         // half the blocks per tile)
         constexpr int DS = MR_COOC_DS;
         typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
-#if MR_COOC_DOT
-        // Σ_d c_d(s) · q_d with q_d cut into 16-bit limbs (q <= 2^40: <= 3):
-        // per song and PAIR of rows one v_perm_b32 packs the two count bytes
-        // as u16 halves and one v_dot2_u32_u16 per limb adds c_A q_A,k +
-        // c_B q_B,k into a u32 limb sum (<= 2^25 per dot, flushed into the
-        // u64 sums every kDotFlush pairs) — the 64-bit multiply-adds (two
-        // v_mad_u64_u32 per song and row) were the dense pass's VALU.
-        // Integer-exact: the same sums.
-        typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
-        constexpr int kDotFlush = 64;  // pairs: 64 x 2^25 < 2^32
-        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
-          unsigned long long aa[DS];
-          unsigned lm[DS][3];
-#pragma unroll
-          for (int i = 0; i < DS; ++i) {
-            aa[i] = 0ull;
-            lm[i][0] = lm[i][1] = lm[i][2] = 0u;
-          }
-          int since = 0;
-          for (int d0 = 0; d0 < nd; d0 += 4) {
-            dvec_t v0[4];
-            unsigned long long qd[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int d = d0 + j;
-              qd[j] = 0ull;
-              v0[j] = dvec_t(0u);
-              if (d < nd) {
-                qd[j] = d_q[d];
-                v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + d_off[d] + (b0 >> 2));
-              }
-            }
-            // the limbs of the four weights: wave-uniform (scalar registers)
-            unsigned ql[4][2];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              ql[j][0] = __builtin_amdgcn_readfirstlane((unsigned)qd[j]);
-              ql[j][1] = __builtin_amdgcn_readfirstlane((unsigned)(qd[j] >> 32));
-            }
-            const unsigned qor = ql[0][1] | ql[1][1] | ql[2][1] | ql[3][1];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {  // row pairs (d0, d0 + 1), (d0 + 2, d0 + 3)
-              const int A = 2 * h, B = 2 * h + 1;
-              const unsigned Q0 = (ql[A][0] & 0xffffu) | (ql[B][0] << 16);
-              const unsigned Q1 = (ql[A][0] >> 16) | (ql[B][0] & 0xffff0000u);
-              const unsigned Q2 = (ql[A][1] & 0xffffu) | (ql[B][1] << 16);
-#pragma unroll
-              for (int i = 0; i < DS; ++i) {
-                const unsigned b = (unsigned)(i & 3);
-                // bytes: A's count, 0, B's count, 0 (perm: 4..7 = src0, 0..3 = src1, 12 = 0x00)
-                const unsigned pk = __builtin_amdgcn_perm(v0[A][i >> 2], v0[B][i >> 2],
-                                                          (4u + b) | (0x0cu << 8) | (b << 16) | (0x0cu << 24));
-                const us2_t P = __builtin_bit_cast(us2_t, pk);
-                lm[i][0] = __builtin_amdgcn_udot2(P, __builtin_bit_cast(us2_t, Q0), lm[i][0], false);
-                lm[i][1] = __builtin_amdgcn_udot2(P, __builtin_bit_cast(us2_t, Q1), lm[i][1], false);
-                if (qor) lm[i][2] = __builtin_amdgcn_udot2(P, __builtin_bit_cast(us2_t, Q2), lm[i][2], false);
-              }
-            }
-            since += 2;
-            if (since >= kDotFlush || d0 + 4 >= nd) {
-#pragma unroll
-              for (int i = 0; i < DS; ++i) {
-                aa[i] += (unsigned long long)lm[i][0] + ((unsigned long long)lm[i][1] << 16) +
-                         ((unsigned long long)lm[i][2] << 32);
-                lm[i][0] = lm[i][1] = lm[i][2] = 0u;
-              }
-              since = 0;
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < DS; ++i)
-            if (b0 + i < bw) acc[b0 + i] += aa[i];
-        }
-#else
         for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
           unsigned long long aa[DS];
 #pragma unroll
@@ -1947,7 +1870,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           for (int i = 0; i < DS; ++i)
             if (b0 + i < bw) acc[b0 + i] += aa[i];
         }
-#endif
         __syncthreads();  // the sparse walk's atomics may hit any song
       }
       MR_STAMP(13);  // dense rows summed
