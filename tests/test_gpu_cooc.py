@@ -63,8 +63,13 @@ BUILD_PATHS = {
     # groups (k_cooc_group, the default whenever the per-user records fit)
     "pertile": {"MR_COOC_LIGHT": "0", "MR_COOC_GROUP": "0"},
     "pertile_dense16": {"MR_COOC_LIGHT": "0", "MR_COOC_GROUP": "0", "MR_COOC_DENSE_DIV": "1000000"},
+    # k_cooc_group with 512-thread workgroups and 2-tile groups: more groups per
+    # row, and rows over 2048 listeners back on the per-group rows_walk (the
+    # pipelined walk holds <= 4 listeners per lane group)
+    "group512": {"MR_COOC_LIGHT": "0", "MR_COOC_GNT": "512", "MR_COOC_GRP": "2"},
 }
-COOC_ENV = ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT", "MR_COOC_GROUP")
+COOC_ENV = ("MR_COOC_LIGHT", "MR_COOC_DENSE_DIV", "MR_COOC_DENSE32", "MR_COOC_SAT", "MR_COOC_GROUP",
+            "MR_COOC_GNT", "MR_COOC_GRP")
 
 
 @pytest.fixture(params=list(BUILD_PATHS))
