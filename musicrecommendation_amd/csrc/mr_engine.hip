@@ -3446,7 +3446,7 @@ int merge_rows_opt() {
 // for k_cooc_group to hold ALL its tiles in one pass (C4 over 8 GPUs: 3 tiles
 // of 15.6k songs): then one listener walk with fire-and-forget counter adds
 // beats hashing for the larger rows, and light rows stop at kLightSlotsNarrow.
-constexpr int64_t kLightSlotsNarrow = 16384;
+constexpr int64_t kLightSlotsNarrow = 8192;  // C4 8 x 1: 6.20 vs 6.32 ms (16k), profiles/r04/s20
 int64_t cooc_light_max_opt(bool narrow) {
   const char* e = std::getenv("MR_COOC_LIGHT_MAX");
   int64_t v = e ? std::atoll(e) : (narrow ? kLightSlotsNarrow : kLightSlots);
