@@ -224,6 +224,10 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   return x;
 }
 
+// Lane `l`'s value to the whole wave through a scalar register (v_readlane:
+// no LDS round trip, unlike __shfl's ds_bpermute). Every lane must be active.
+__device__ __forceinline__ int wave_lane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
 // Block-wide exclusive scan of one int per thread (256 threads). `sbuf` holds kWaves ints.
 __device__ __forceinline__ int block_excl_scan(int x, int* total, int* sbuf) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2219,7 +2223,7 @@ __device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int ti
       }
       int base = 0;
       if (lane == 0 && nz > 0) base = atomicAdd(s_tail, nz);
-      base = __shfl(base, 0, 64);
+      base = wave_lane(base, 0);
       for (int i0 = wb; i0 < we; i0 += 64) {
         const int i = i0 + lane;
         const unsigned c = i < we ? count_of(i) : 0u;
@@ -2566,7 +2570,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
         p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
         p.seg_len[(size_t)t * p.n_rows + r] = c;
       }
-      run += __shfl(inc, 63, 64);
+      run += wave_lane(inc, 63);
     }
   }
   __syncthreads();
@@ -2637,7 +2641,7 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
         p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
         p.seg_len[(size_t)t * p.n_rows + r] = c;
       }
-      run += __shfl(inc, 63, 64);
+      run += wave_lane(inc, 63);
     }
     if (lane == 0) p.row_nnz[r] = (unsigned)run;
   }
@@ -2670,7 +2674,8 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
 // C4 (107 GB of fetches per step for ~6 GB of entries).
 constexpr int kMaxGroupTiles = 8;
 __host__ __device__ inline int cooc_group_lds(int bs, int g) {
-  return align16(g * bs * 2) + 3 * kMaxGroupTiles * 4;  // counters; per tile: total, cursor, excess
+  // counters; per tile: excess entries (+ spare words); per (tile, wave): non-zeros
+  return align16(g * bs * 2) + 3 * kMaxGroupTiles * 4 + kMaxGroupTiles * 16 * 4;
 }
 
 // Bit 15 / bit 31 of the result set iff the low / high u16 half of x is non-zero
@@ -2687,35 +2692,50 @@ __device__ __forceinline__ int nz_pairs8(const uint4& w) {
 
 // All tiles [t0, t0 + ntg) of a k_cooc_group pass written from their u16
 // counters (tile k's at cnt + k * bs / 2): pass A counts every tile's
-// non-zeros (16-B LDS chunks, one LDS add per wave and tile), ONE barrier,
-// then every thread derives the same segment offsets — a sparse segment its
-// non-zeros, a dense one its count bytes plus room for as many excess entries
-// as it has non-zeros (an upper bound: within the row's pool bound, see
-// mr_load), so no tile waits for the previous tile's excess count — pass B
-// writes every tile (dense: count bytes + excess entries; sparse: compaction
-// at DPP-scanned wave prefixes, one LDS add per wave and chunk row), ONE
-// barrier, and thread 0 records the segments. s_tot / s_cur / s_tail [ntg]
-// are zero on entry. Advances *off (rows at a running offset) and *row_nz.
+// non-zeros per WAVE (16-B LDS chunks, the wave's sum to s_wcnt[k][w], no
+// atomics), ONE barrier, then every thread derives the same segment offsets
+// from those sums — a sparse segment its non-zeros, a dense one its count
+// bytes plus room for as many excess entries as it has non-zeros (an upper
+// bound: within the row's pool bound, see mr_load), so no tile waits for the
+// previous tile's excess count — and its wave's start inside each segment
+// (the waves before it: pass B visits the same chunks as pass A); pass B
+// writes every tile (dense: count bytes + excess entries; sparse: each wave
+// compacts at DPP-scanned prefixes from its own start, no LDS cursor), ONE
+// barrier, and thread 0 records the segments. s_tail [ntg] is zero on entry;
+// every wave writes its s_wcnt entries. Advances *off (rows at a running
+// offset) and *row_nz. (The per-wave starts replace an LDS atomic on one
+// cursor word per wave and chunk row, which the 16 waves serialized on.)
 template <int NT>
 __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bool big, int t0, int ntg, int bs,
-                                                  int width, const unsigned* cnt, int* s_tot, int* s_cur, int* s_tail,
+                                                  int width, const unsigned* cnt, int* s_wcnt, int* s_tail,
                                                   long long* off, unsigned* row_nz) {
-  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int k = 0; k < ntg; ++k) {
     const int bw = min(width, (t0 + k + 1) * bs) - (t0 + k) * bs;
     const uint4* cv = reinterpret_cast<const uint4*>(cnt + (size_t)k * (bs >> 1));
     const int nch = (bw + 7) >> 3;
     int nz = 0;
     for (int c = tid; c < nch; c += NT) nz += nz_pairs8(cv[c]);
-    const int ws = __shfl(wave_incl_scan(nz), 63, 64);
-    if (lane == 0 && ws) atomicAdd(&s_tot[k], ws);
+    const int ws = wave_lane(wave_incl_scan(nz), 63);
+    if (lane == 0) s_wcnt[k * NW + w] = ws;
   }
   __syncthreads();
+  // tile k's non-zeros, and this wave's first entry among them (lane x reads
+  // wave x's count; one scan, two lane reads)
+  const int ws_id = __builtin_amdgcn_readfirstlane(w);
+  auto tile_counts = [&](int k, int& total, int& wbase) {
+    const int c = lane < NW ? s_wcnt[k * NW + lane] : 0;
+    const int inc = wave_incl_scan(c);
+    total = wave_lane(inc, 63);
+    wbase = wave_lane(inc - c, ws_id);
+  };
   long long o = *off;
   for (int k = 0; k < ntg; ++k) {
     const int tile = t0 + k;
     const int bw = min(width, (tile + 1) * bs) - tile * bs;
-    const int total = s_tot[k];
+    int total, wbase;
+    tile_counts(k, total, wbase);
     const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
 #if MR_GROUP_STUB == 2  // timing-only build: pass A only
     if (!big) o += dense ? ((cooc_dense_words(bw) + total + 3) & ~3) : ((total + 3) & ~3);
@@ -2741,17 +2761,16 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     } else {
       const uint4* cv = reinterpret_cast<const uint4*>(cw);
       const int nch = (bw + 7) >> 3;
+      unsigned run = (unsigned)wbase;  // this wave's next entry
       for (int c0 = 0; c0 < nch; c0 += NT) {  // wave-uniform trip count (scans inside)
         const int c = c0 + tid;
-        uint4 w = make_uint4(0u, 0u, 0u, 0u);
-        if (c < nch) w = cv[c];
-        const int n = nz_pairs8(w);  // (w is zero past the tile)
+        uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
+        if (c < nch) w4 = cv[c];
+        const int n = nz_pairs8(w4);  // (zero past the tile)
         const int incl = wave_incl_scan(n);
-        const int wtot = __shfl(incl, 63, 64);
-        int base = 0;
-        if (lane == 0 && wtot) base = atomicAdd(&s_cur[k], wtot);
-        unsigned pos = (unsigned)(__shfl(base, 0, 64) + incl - n);
-        const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+        unsigned pos = run + (unsigned)(incl - n);
+        run += (unsigned)wave_lane(incl, 63);
+        const unsigned ww[4] = {w4.x, w4.y, w4.z, w4.w};
         const unsigned key0 = (unsigned)(c * 8) << kCoocCntBits;
 #if MR_GROUP_STUB != 1  // (1: timing-only build without the sparse stores)
 #pragma unroll
@@ -2760,7 +2779,7 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
           if (v) out[pos++] = (key0 | ((unsigned)i << kCoocCntBits)) | v;
         }
 #else
-        if (base < 0) out[0] = ww[0];
+        if ((int)pos < 0) out[0] = ww[0];
 #endif
       }
     }
@@ -2773,7 +2792,8 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     for (int k = 0; k < ntg; ++k) {
       const int tile = t0 + k;
       const int bw = min(width, (tile + 1) * bs) - tile * bs;
-      const int total = s_tot[k];
+      int total = 0;
+      for (int x = 0; x < NW; ++x) total += s_wcnt[k * NW + x];
       const bool dense = p.dense_div > 0 && (long long)total * p.dense_div >= bw;
       p.seg_off[(size_t)tile * p.n_rows + r] = big ? p.row_base[r] + (long long)tile * p.tcap : q;
       p.seg_len[(size_t)tile * p.n_rows + r] = dense ? kCoocDenseTail - s_tail[k] : total;
@@ -2797,13 +2817,13 @@ struct GroupRange {
 };
 
 // A k_cooc_group pass's counters zeroed up to the last 16-B chunk's end (the
-// emission's chunk counts need no bound test), and its per-tile totals,
-// cursors and excess counters.
+// emission's chunk counts need no bound test), and its per-tile excess
+// counters.
 template <int NT>
-__device__ __forceinline__ void group_zero(unsigned* cnt, int gw, int* s_tot) {
+__device__ __forceinline__ void group_zero(unsigned* cnt, int gw, int* s_tail) {
   uint4* c4 = reinterpret_cast<uint4*>(cnt);
   for (int i = threadIdx.x; i < (gw + 7) >> 3; i += NT) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (threadIdx.x < 3 * kMaxGroupTiles) s_tot[threadIdx.x] = 0;
+  if (threadIdx.x < kMaxGroupTiles) s_tail[threadIdx.x] = 0;
 }
 
 // Entries x .. x + 3 of sr_songs below b (a prefix of the chunk) or none.
@@ -2843,7 +2863,7 @@ __device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int 
 constexpr int kGroupPipeR = 4;
 template <int NT>
 __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const int* lst, int n, int glog,
-                                                     int width, unsigned* cnt, int* s_tot, int* s_cur, int* s_tail,
+                                                     int width, unsigned* cnt, int* s_wcnt, int* s_tail,
                                                      long long* sb, long long* off, unsigned* row_nz) {
   constexpr int R = kGroupPipeR;
   const int tid = threadIdx.x;
@@ -2882,7 +2902,7 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
     const int t0 = gi * GT, t1 = min(nt, t0 + GT), t2 = min(nt, t1 + GT);
     const unsigned lo0 = (unsigned)(t0 * bs);  // shard-local first song of the group
     const int gw = min(width, t1 * bs) - t0 * bs;
-    group_zero<NT>(cnt, gw, s_tot);
+    group_zero<NT>(cnt, gw, s_tail);
     // the next group's end (its start is this group's end)
     unsigned e[R];
 #pragma unroll
@@ -2919,8 +2939,8 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
         m[i][1] = group_chunk(songs, x + 4u * L, b[i], c[i][1]);
       }
     }
-    cooc_emit_group16<NT>(p, r, false, t0, t1 - t0, bs, width, cnt, s_tot, s_cur, s_tail, off, row_nz);
-    // thread 0 reads s_tot / s_tail after the emission's closing barrier: keep
+    cooc_emit_group16<NT>(p, r, false, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, off, row_nz);
+    // thread 0 reads s_wcnt / s_tail after the emission's closing barrier: keep
     // the next group's zeroing behind it
     __syncthreads();
     if (gi == 0) stamp_rt(sb, 2);  // the first group's tiles emitted
@@ -2933,9 +2953,8 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   const int bs = p.block_songs, G = p.grp, ng = p.n_grp;
   const int width = p.song_hi - p.song_lo;
   unsigned* cnt = reinterpret_cast<unsigned*>(smem_raw);
-  int* s_tot = reinterpret_cast<int*>(smem_raw + align16(G * bs * 2));  // [grp] non-zeros per tile
-  int* s_cur = s_tot + kMaxGroupTiles;       // [grp] compaction cursors
-  int* s_tail = s_cur + kMaxGroupTiles;      // [grp] excess entries per dense tile
+  int* s_tail = reinterpret_cast<int*>(smem_raw + align16(G * bs * 2));  // [grp] excess entries per dense tile
+  int* s_wcnt = s_tail + 3 * kMaxGroupTiles;  // [grp][NT / 64] non-zeros per tile and wave
   const int tid = threadIdx.x;
   // big rows (the first n_big): one workgroup per (row, group), a row's groups
   // on one XCD (blocks are dealt round-robin over the 8 XCDs: slot k of XCD x
@@ -2968,7 +2987,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   unsigned row_nz = 0u;
 #if MR_GROUP_PIPE
   if (!big && n <= (NT >> glog) * kGroupPipeR) {
-    cooc_group_pipelined<NT>(p, r, lst, n, glog, width, cnt, s_tot, s_cur, s_tail, sb, &off, &row_nz);
+    cooc_group_pipelined<NT>(p, r, lst, n, glog, width, cnt, s_wcnt, s_tail, sb, &off, &row_nz);
     g_end = g_begin;  // (every group done)
   }
 #endif
@@ -2976,7 +2995,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     const int t0 = gi * G, t1 = min(p.n_tiles, t0 + G);
     const int lo0 = t0 * bs;  // shard-local first song of the group
     const int gw = min(width, t1 * bs) - lo0;
-    group_zero<NT>(cnt, gw, s_tot);
+    group_zero<NT>(cnt, gw, s_tail);
     __syncthreads();
     // fire-and-forget adds (no returned value, no per-entry bookkeeping)
     rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs,
@@ -2991,8 +3010,8 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
     // tile k's counters start at word k * bs / 2 (bs is a multiple of 256: 16-B aligned)
-    cooc_emit_group16<NT>(p, r, big, t0, t1 - t0, bs, width, cnt, s_tot, s_cur, s_tail, &off, &row_nz);
-    // thread 0 reads s_tot / s_tail after the emission's closing barrier: keep
+    cooc_emit_group16<NT>(p, r, big, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, &off, &row_nz);
+    // thread 0 reads s_wcnt / s_tail after the emission's closing barrier: keep
     // the next group's zeroing behind it (the dc4df36 race class)
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 2);  // the first group's tiles emitted
