@@ -2390,41 +2390,9 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
 #ifndef MR_WALK_R
 #define MR_WALK_R 2  // listeners per lane group per iteration of rows_walk (loads issued together)
 #endif
-// rows_walk in three parts, so a caller can issue the next row's first loads
-// early (k_cooc_light: a workgroup's next row's listener ids during this
-// row's walk, their row ranges during this row's emission):
-// rows_walk_ids — this lane group's first listener ids (iteration 0 and 1);
-// rows_walk_ranges — iteration 0's row ranges from them; rows_walk_run — the
-// software-pipelined walk from there.
-struct WalkIds {
-  int v0[MR_WALK_R], v1[MR_WALK_R];
-};
-struct WalkHead {
-  long long a0[MR_WALK_R], b0[MR_WALK_R];
-  int v1[MR_WALK_R];
-};
-__device__ __forceinline__ void rows_walk_ids(int lane_id, int n_lanes, int glog, const int* lst, int n, WalkIds& w) {
-  constexpr int R = MR_WALK_R;
-  const int grp = lane_id >> glog, step = n_lanes >> glog, stride = step * R;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int l = grp + r * step, l1 = l + stride;
-    w.v0[r] = l < n ? lst[l] : -1;
-    w.v1[r] = l1 < n ? lst[l1] : -1;
-  }
-}
-template <typename Range>
-__device__ __forceinline__ void rows_walk_ranges(const WalkIds& w, Range&& range, WalkHead& h) {
-#pragma unroll
-  for (int r = 0; r < MR_WALK_R; ++r) {
-    h.a0[r] = h.b0[r] = 0;
-    if (w.v0[r] >= 0) range(w.v0[r], h.a0[r], h.b0[r]);
-    h.v1[r] = w.v1[r];
-  }
-}
 template <typename Range, typename Ins>
-__device__ __forceinline__ void rows_walk_run(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
-                                              const unsigned* sr_songs, Ins&& ins, WalkHead& h) {
+__device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
+                                          const unsigned* sr_songs, Ins&& ins) {
   constexpr int R = MR_WALK_R;
   const int G = 1 << glog;
   const int grp = lane_id >> glog, j = lane_id & (G - 1);
@@ -2447,9 +2415,15 @@ __device__ __forceinline__ void rows_walk_run(int lane_id, int n_lanes, int glog
   // iteration i: listeners grp + i * stride + r * step, r < R; the next
   // iteration's row ranges and the one after's ids are loaded while this
   // iteration's first chunks are inserted
-  long long* a0 = h.a0;
-  long long* b0 = h.b0;
-  int* v1 = h.v1;
+  long long a0[R], b0[R];
+  int v1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int l = grp + r * step, l1 = l + stride;
+    a0[r] = b0[r] = 0;
+    if (l < n) range(lst[l], a0[r], b0[r]);
+    v1[r] = l1 < n ? lst[l1] : -1;
+  }
   for (int l0 = grp; l0 < n; l0 += stride) {
     u32x4_a4 c[R][2];
     int m[R][2];
@@ -2485,15 +2459,6 @@ __device__ __forceinline__ void rows_walk_run(int lane_id, int n_lanes, int glog
       v1[r] = v2[r];
     }
   }
-}
-template <typename Range, typename Ins>
-__device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
-                                          const unsigned* sr_songs, Ins&& ins) {
-  WalkIds w;
-  WalkHead h;
-  rows_walk_ids(lane_id, n_lanes, glog, lst, n, w);
-  rows_walk_ranges(w, range, h);
-  rows_walk_run(lane_id, n_lanes, glog, lst, n, range, sr_songs, ins, h);
 }
 
 // A lane's batch of keys (k[0 .. m), m <= 8) into a light row's table as a
@@ -2549,121 +2514,81 @@ struct ShardRow {
 };
 __device__ __forceinline__ ShardRow shard_row(const CoocParams& p) { return ShardRow{p.sr_off}; }
 
-// Light index rows: a workgroup per kLightRowsPerBlock rows (each row whole,
-// instead of one workgroup per (row, tile)).
+// Light index rows: one workgroup per row (instead of one per (row, tile)).
 // The row's listeners' whole shard rows (sr_off / sr_songs) are walked by
 // listener (rows_walk: groups of lanes per listener) into an LDS hash table
 // of counts (light_insert), then the table is emitted tile by tile: per-tile
 // counts, their prefix -> the row's segment of every tile (seg_off / seg_len,
 // empty tiles included), entries placed by LDS cursors (order inside a
 // segment is arbitrary; the consumer's sums are order-free).
-// kLightRowsPerBlock rows per workgroup (rows blockIdx.x + k * gridDim.x, so
-// every workgroup gets a like mix of the tier's size-sorted rows), pipelined:
-// the next row's listener ids are loaded while this row is walked and their
-// row ranges while this row is emitted, so a row's walk starts with its first
-// chunks' addresses in hand instead of two dependent loads (~3-5 us each
-// under load) after the previous row.
-#ifndef MR_LIGHT_ROWS
-#define MR_LIGHT_ROWS 4
-#endif
-constexpr int kLightRowsPerBlock = MR_LIGHT_ROWS;
 template <int NT, int SMAX>
-__global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p, int n_launch) {
+__global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   using Lay = LightLds<NT, SMAX>;
-  constexpr int K = kLightRowsPerBlock;
   unsigned* tab = reinterpret_cast<unsigned*>(smem_raw + Lay::tab);
   int* tcnt = reinterpret_cast<int*>(smem_raw + Lay::tcnt);
   int* tpos = reinterpret_cast<int*>(smem_raw + Lay::tpos);
+  const int4 rd = p.rdesc[blockIdx.x];  // {row, slots | lane-group log2, listener list start, listeners}
+  const int r = rd.x;
   const int tid = threadIdx.x;
+  long long* sb = p.lstamps ? p.lstamps + (size_t)blockIdx.x * 8 : nullptr;
+  stamp_rt(sb, 0);
+  const int S = rd.y & kLightSlotsMask;
+  const unsigned mask = (unsigned)S - 1u;
+  const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
+  for (int i = tid; i < S; i += NT) tab[i] = 0u;
+  for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
+  const int n = rd.w;
+  const int* lst = p.trs_users + (unsigned)rd.z;
+  __syncthreads();  // the table and the tile counters are zero
+  stamp_rt(sb, 1);
+  rows_walk(tid, NT, rd.y >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+            [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
+  __syncthreads();
+  stamp_rt(sb, 2);
+  // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
-  // {row, slots | lane-group log2, listener list start, listeners} of each row
-  int4 rd[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int ri = blockIdx.x + k * gridDim.x;
-    rd[k] = ri < n_launch ? p.rdesc[ri] : make_int4(-1, 0, 0, 0);
+  for (int i = tid; i < S; i += NT) {
+    const unsigned x = tab[i];
+    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
   }
-  WalkIds ids;
-  WalkHead h;
-  rows_walk_ids(tid, NT, rd[0].y >> kLightGlogShift, p.trs_users + (unsigned)rd[0].z, rd[0].w, ids);
-  rows_walk_ranges(ids, shard_row(p), h);
-  int4 cur = rd[0];
-#pragma unroll 1
-  for (int k = 0; k < K; ++k) {
-    if (cur.x < 0) break;  // (uniform: the rows past the launch)
-    const int r = cur.x;
-    const int ri = blockIdx.x + k * gridDim.x;
-    long long* sb = p.lstamps ? p.lstamps + (size_t)ri * 8 : nullptr;
-    stamp_rt(sb, 0);
-    const int S = cur.y & kLightSlotsMask;
-    const unsigned mask = (unsigned)S - 1u;
-    const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
-    for (int i = tid; i < S; i += NT) tab[i] = 0u;
-    for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
-    const int n = cur.w;
-    const int glog = cur.y >> kLightGlogShift;
-    const int* lst = p.trs_users + (unsigned)cur.z;
-    // the next row's listener ids, in flight during this row's walk (rd[k + 1]
-    // picked by compares: no dynamic register indexing)
-    int4 nrd = make_int4(-1, 0, 0, 0);
-#pragma unroll
-    for (int q = 0; q < K; ++q)
-      if (q == k + 1) nrd = rd[q];
-    WalkIds nids;
-    if (nrd.x >= 0) rows_walk_ids(tid, NT, nrd.y >> kLightGlogShift, p.trs_users + (unsigned)nrd.z, nrd.w, nids);
-    __syncthreads();  // the table and the tile counters are zero
-    stamp_rt(sb, 1);
-    rows_walk_run(tid, NT, glog, lst, n, shard_row(p), p.sr_songs,
-                  [&](const unsigned (&kk)[8], int m) { light_insert_queue(tab, mask, sh, kk, m); }, h);
-    __syncthreads();
-    stamp_rt(sb, 2);
-    // the next row's ranges, in flight during this row's emission
-    if (nrd.x >= 0) rows_walk_ranges(nids, shard_row(p), h);
-    // emit: per-tile counts, segment offsets, then the entries
-    for (int i = tid; i < S; i += NT) {
-      const unsigned x = tab[i];
-      if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
+  __syncthreads();
+  stamp_rt(sb, 3);
+  if (tid < 64) {  // prefix over <= kLightMaxTiles tiles by one wave
+    int run = 0;
+    if (tid == 0) {
+      int nz = 0;
+      for (int t = 0; t < p.n_tiles; ++t) nz += tcnt[t];
+      p.row_nnz[r] = (unsigned)nz;
     }
-    __syncthreads();
-    stamp_rt(sb, 3);
-    if (tid < 64) {  // prefix over <= kLightMaxTiles tiles by one wave
-      int run = 0;
-      if (tid == 0) {
-        int nz = 0;
-        for (int t = 0; t < p.n_tiles; ++t) nz += tcnt[t];
-        p.row_nnz[r] = (unsigned)nz;
+    for (int t0 = 0; t0 < p.n_tiles; t0 += 64) {
+      const int t = t0 + tid;
+      const int c = t < p.n_tiles ? tcnt[t] : 0;
+      const int inc = wave_incl_scan(c);
+      if (t < p.n_tiles) {
+        tpos[t] = run + inc - c;
+        p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
+        p.seg_len[(size_t)t * p.n_rows + r] = c;
       }
-      for (int t0 = 0; t0 < p.n_tiles; t0 += 64) {
-        const int t = t0 + tid;
-        const int c = t < p.n_tiles ? tcnt[t] : 0;
-        const int inc = wave_incl_scan(c);
-        if (t < p.n_tiles) {
-          tpos[t] = run + inc - c;
-          p.seg_off[(size_t)t * p.n_rows + r] = p.row_base[r] + run + inc - c;
-          p.seg_len[(size_t)t * p.n_rows + r] = c;
-        }
-        run += wave_lane(inc, 63);
-      }
+      run += wave_lane(inc, 63);
     }
-    __syncthreads();
-    unsigned* out = p.pool + p.row_base[r];
-    for (int i = tid; i < S; i += NT) {
-      const unsigned x = tab[i];
-      if (x) {
-        const int key = (int)((x >> kLightCntBits) - 1u);
-        const int t = key / bs;
-        const int pos = atomicAdd(&tpos[t], 1);
-        out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
-      }
-    }
-    __syncthreads();  // (the next row rezeroes the table)
-    stamp_rt(sb, 4);
-    stamp_val(sb, 5, n);
-    stamp_val(sb, 6, S);
-    stamp_val(sb, 7, NT);
-    cur = nrd;
   }
+  __syncthreads();
+  unsigned* out = p.pool + p.row_base[r];
+  for (int i = tid; i < S; i += NT) {
+    const unsigned x = tab[i];
+    if (x) {
+      const int key = (int)((x >> kLightCntBits) - 1u);
+      const int t = key / bs;
+      const int pos = atomicAdd(&tpos[t], 1);
+      out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
+    }
+  }
+  __syncthreads();
+  stamp_rt(sb, 4);
+  stamp_val(sb, 5, n);
+  stamp_val(sb, 6, S);
+  stamp_val(sb, 7, NT);
 }
 
 // The smallest light rows, one wave per row (kWaveRowsPerBlock rows per
@@ -3134,8 +3059,7 @@ int light_tier_go(hipStream_t st, int n, const CoocParams* lp) {
     MR_HIP(hipFuncSetAttribute((const void*)k_cooc_light<NT, S>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     return MR_OK;
   }
-  hipLaunchKernelGGL((k_cooc_light<NT, S>), dim3((n + kLightRowsPerBlock - 1) / kLightRowsPerBlock), dim3(NT),
-                     (size_t)lds, st, *lp, n);
+  hipLaunchKernelGGL((k_cooc_light<NT, S>), dim3(n), dim3(NT), (size_t)lds, st, *lp);
   MR_HIP(hipGetLastError());
   return MR_OK;
 }
