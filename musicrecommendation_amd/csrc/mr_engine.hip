@@ -3763,22 +3763,12 @@ int mr_create(const mr_options* opt, mr_ctx** out) {
   MR_HIP(hipSetDevice(o.device));
   mr_ctx* c = new mr_ctx();
   c->opt = o;
-  // Stream priorities (MR_STREAM_PRIO, A/B): 1 = the context stream (heavy
-  // index rows, scoring) above the light rows' side streams, 2 = the side
-  // streams above it, else all at the default priority.
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  const char* pe = std::getenv("MR_STREAM_PRIO");
-  const int pmode = pe ? std::atoi(pe) : 0;
-  hipError_t e = pmode == 1 ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi)
-                            : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
     return fail(MR_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
-  for (int i = 0; i < 2 && e == hipSuccess; ++i)
-    e = pmode == 2 ? hipStreamCreateWithPriority(&c->side[i], hipStreamNonBlocking, prio_hi)
-                   : hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming);
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->side_join[i], hipEventDisableTiming);
   if (e != hipSuccess) {
