@@ -1580,6 +1580,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
+#ifndef MR_COOC_DPF
+#define MR_COOC_DPF 1       // co-listening scoring: the first descriptor pass's row lookups issued before the zeroing
+#endif
 #ifndef MR_COOC_PF
 #define MR_COOC_PF 0        // co-listening scoring: per-song scales prefetched per thread (songs tid + NT e;
                             // 0 = none)
@@ -1764,7 +1767,29 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       scp[e] = i < bw ? p.sqrt_c[blo + i] : 1.0;
     }
   }
+  // co-listening route: the first descriptor pass's row lookups (te_row /
+  // te_songs, then seg_len / seg_off / q_song) issued around the zeroing and
+  // the heard bitmap instead of after them (two dependent loads off the
+  // descriptor phase's critical path)
+  constexpr bool kDPF = COOC && MR_COOC_DPF;
+  int pf_r = -1, pf_s = 0, pf_sl = 0;
+  long long pf_off = 0;
+  unsigned long long pf_q = 0ull;
+  if constexpr (kDPF) {
+    const long long a = p.te_off[u];
+    if (tid < min<long long>(p.nseg, p.te_off[u + 1] - a)) {
+      pf_r = p.te_row[a + tid];
+      pf_s = p.te_songs[a + tid];
+    }
+  }
   for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
+  if constexpr (kDPF) {
+    if (pf_r >= 0) {
+      pf_sl = p.seg_len[(size_t)tile * p.n_rows + pf_r];
+      pf_off = p.seg_off[(size_t)tile * p.n_rows + pf_r];
+      pf_q = (unsigned long long)p.q_song[pf_s];
+    }
+  }
   for (int i = tid; i < bs / 32; i += NT) heard[i] = 0u;
   __syncthreads();
   for (long long i = p.te_off[u] + tid; i < p.te_off[u + 1]; i += NT) {
@@ -1809,11 +1834,21 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       long long off = 0, tail_off = -1;
       unsigned long long q = 0ull;
       if (tid < ns) {
-        const int r = p.te_row[c0 + tid];
+        int r, sl = 0;
+        if (kDPF && c0 == t0) {  // (prefetched above)
+          r = pf_r;
+          sl = pf_sl;
+          off = pf_off;
+          q = pf_q;
+        } else {
+          r = p.te_row[c0 + tid];
+          if (r >= 0) {
+            sl = slen[r];
+            off = soff[r];
+            q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
+          }
+        }
         if (r >= 0) {
-          const int sl = slen[r];
-          off = soff[r];
-          q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
           if (sl < 0) {  // saturated count bytes, then the excess entries
             isd = 1;
             fmt = sl;
