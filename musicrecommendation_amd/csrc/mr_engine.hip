@@ -1558,9 +1558,10 @@ __host__ __device__ inline WideLds<NT> wide_lds(int bs, int k, int n_chunks) {
 
 constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_R
-#define MR_WIDE_R 2         // neighbours per thread per iteration (wide kernel; with the 3-level software
-                            // pipeline 2 beats 4 by 2 % at C4 and a next-list-only prefetch loses,
-                            // profiles/r02/c4/pipeline_ab.txt)
+#define MR_WIDE_R 4         // neighbours per thread per iteration (wide kernel, 3-level software pipeline):
+                            // 4 vs 2 at C5's ubm model 61.7 vs 66.0 ms, C3 1.108 vs 1.119 ms (ibm) —
+                            // 3: 63.1, 6: 71.0, 8 spills (profiles/r04/s27, s28; round 2 measured 2
+                            // ahead by 2 % at C4 on an older kernel, profiles/r02/c4/pipeline_ab.txt)
 #endif
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
