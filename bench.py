@@ -267,8 +267,9 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
 
     def step():
         ubm, ibm = ens.model("ubm"), ens.model("ibm")
-        models = {"ubm": ubm, "ibm": ibm, "lcm": ens.linear(ubm, ibm, 0.5), "am": ens.aggregation(ubm, ibm, 0.5),
-                  "scm": ens.stochastic(ubm, ibm, 0.5, seed=1)}
+        # the three combinations in one pass, their min / max carried to threshold_map
+        lcm, am, scm = ens.combinations(ubm, ibm, 0.5, 0.5, 0.5, seed=1)
+        models = {"ubm": ubm, "ibm": ibm, "lcm": lcm, "am": am, "scm": scm}
         for name, t in models.items():
             maps[name] = ens.threshold_map(t)
         return models
@@ -302,8 +303,9 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         if eng.ibm_route == "cooc":  # the ibm model's byte model on its route (counts of the last ibm run)
             ibm_bytes = sum(cooc_bytes(eng, ds, 4, 10).values())
         dense_elems = full.n_test * full.n_songs
-        # per step: 2 models + 3 combinations (2 reads + 1 write) + 5 x (min/max read + counts read)
-        step_bytes = model_bytes + ibm_bytes + dense_elems * 4 * (3 * 3 + 5 * 2)
+        # per step: 2 models + the combinations' one pass (2 reads + 3 writes) + min/max reads of the
+        # 2 models (the combinations carry theirs) + 5 counts reads
+        step_bytes = model_bytes + ibm_bytes + dense_elems * 4 * (2 + 3 + 2 + 5)
         step_s = elapsed / args.steps
         traffic = None
         pmc_file = os.path.join(ROOT, "profiles", "pmc_c5.json")

@@ -335,6 +335,16 @@ int mr_topk_merge_records_async(mr_ctx* ctx, int32_t n_shards, int32_t n_te, int
                                  u = 24-bit uniform of splitmix64(seed + (idx+1)*0x9E3779B97F4A7C15) */
 int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_t pair_base, int64_t n_pairs,
                       const void* ubm, const void* ibm, void* out);
+/* The driver's three combinations (main.scala:57-89) in one pass over ubm and
+ * ibm: out_linear (alpha), out_aggregation (ibm_percentage), out_stochastic
+ * (ibm_probability, seed) — each bit-equal to mr_combine_device of its kind —
+ * and, when minmax is non-null, each output's min / max over its pairs as
+ * minmax[0..5] = {lin min, lin max, agg min, agg max, sto min, sto max} (what
+ * mr_eval_minmax_device returns for it: +inf / -inf when the shard holds no
+ * pair). Replaces MR:317-481 called three times, each reading both models. */
+int mr_combine_all_device(mr_ctx* ctx, double alpha, double ibm_percentage, double ibm_probability, uint64_t seed,
+                          int64_t pair_base, int64_t n_pairs, const void* ubm, const void* ibm, void* out_linear,
+                          void* out_aggregation, void* out_stochastic, double* minmax);
 /* evaluateModel (MR:636), device part: min / max over the model's scores
  * (MR:524-525; +inf / -inf when the shard holds no pair) ... */
 int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx);

@@ -167,6 +167,8 @@ SIGNATURES = {
     "mr_view_get": (c_int, [c_void_p, POINTER(MrView)]),
     "mr_topk_dense_device": (c_int, [c_void_p, c_void_p, c_int32]),
     "mr_combine_device": (c_int, [c_void_p, c_int, c_double, ctypes.c_uint64, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mr_combine_all_device": (c_int, [c_void_p, c_double, c_double, c_double, ctypes.c_uint64, c_int64, c_int64,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_double)]),
     "mr_eval_minmax_device": (c_int, [c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)]),
     "mr_eval_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_int32]),

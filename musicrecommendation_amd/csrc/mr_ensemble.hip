@@ -130,6 +130,119 @@ __global__ __launch_bounds__(kThreads) void k_combine(CombParams p) {
   }
 }
 
+// The driver's three combinations in one pass (mr_combine_all_device): each
+// block reads its ubm / ibm elements once and writes the linear, aggregation
+// and stochastic outputs with k_combine's exact expressions; with part != null
+// it also leaves the min / max of each output over its pairs (NaN skipped, in
+// the element type, as k_minmax) in part[block][6].
+struct Comb3Params {
+  int n_te, width, song_lo, n_songs;
+  double alpha, p_sto;
+  unsigned long long seed;
+  long long pair_base, threshold;
+  const long long* te_off;
+  const int* te_songs;
+  const void* ubm;
+  const void* ibm;
+  void* out[3];  // linear, aggregation, stochastic
+  double* part;
+};
+template <typename OutT>
+__global__ __launch_bounds__(kThreads) void k_combine3(Comb3Params p) {
+  __shared__ double sm[6][kThreads];
+  const int u = blockIdx.y;
+  const int i0 = blockIdx.x * kThreads * kCombPer + threadIdx.x;
+  const size_t row = (size_t)u * p.width;
+  const OutT* ubm = reinterpret_cast<const OutT*>(p.ubm) + row;
+  const OutT* ibm = reinterpret_cast<const OutT*>(p.ibm) + row;
+  OutT* o_lin = reinterpret_cast<OutT*>(p.out[0]) + row;
+  OutT* o_agg = reinterpret_cast<OutT*>(p.out[1]) + row;
+  OutT* o_sto = reinterpret_cast<OutT*>(p.out[2]) + row;
+  OutT a4[kCombPer], b4[kCombPer];
+#pragma unroll
+  for (int r = 0; r < kCombPer; ++r) {
+    const int i = i0 + r * kThreads;
+    a4[r] = i < p.width ? ubm[i] : (OutT)0;
+    b4[r] = i < p.width ? ibm[i] : (OutT)0;
+  }
+  const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  const int s_blk = p.song_lo + blockIdx.x * kThreads * kCombPer;  // first song of the block
+  long long a = t0, b = t1;  // first song of T(u) >= s_blk (uniform over the block)
+  while (a < b) {
+    const long long m = (a + b) >> 1;
+    if (p.te_songs[m] < s_blk) a = m + 1; else b = m;
+  }
+  OutT mn[3], mx[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) { mn[c] = (OutT)INFINITY; mx[c] = (OutT)-INFINITY; }
+  auto track = [&](int c, OutT x) {
+    if (x != x) return;
+    mn[c] = x < mn[c] ? x : mn[c];
+    mx[c] = x > mx[c] ? x : mx[c];
+  };
+#pragma unroll
+  for (int r = 0; r < kCombPer; ++r) {
+    const int i = i0 + r * kThreads;
+    if (i >= p.width) continue;
+    const OutT lin = (OutT)((double)a4[r] * p.alpha + (double)b4[r] * (1.0 - p.alpha));  // MR:327
+    o_lin[i] = lin;
+    track(0, lin);
+    const int s = p.song_lo + i;
+    long long j = a;  // first song of T(u) >= s
+    while (j < t1 && p.te_songs[j] < s) ++j;
+    if (j < t1 && p.te_songs[j] == s) {  // heard: no pair (MR:109)
+      o_agg[i] = (OutT)NAN;
+      o_sto[i] = (OutT)NAN;
+      continue;
+    }
+    const long long idx = p.pair_base + (long long)u * p.n_songs - t0 + s - (j - t0);
+    const OutT agg = idx < p.threshold ? b4[r] : a4[r];                               // MR:380-381
+    const OutT sto = (double)pair_uniform(p.seed, idx) < p.p_sto ? b4[r] : a4[r];     // MR:414-415
+    o_agg[i] = agg;
+    o_sto[i] = sto;
+    track(1, agg);
+    track(2, sto);
+  }
+  if (!p.part) return;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    sm[2 * c][threadIdx.x] = (double)mn[c];
+    sm[2 * c + 1][threadIdx.x] = (double)mx[c];
+  }
+  __syncthreads();
+  for (int h = kThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        sm[2 * c][threadIdx.x] = fmin(sm[2 * c][threadIdx.x], sm[2 * c][threadIdx.x + h]);
+        sm[2 * c + 1][threadIdx.x] = fmax(sm[2 * c + 1][threadIdx.x], sm[2 * c + 1][threadIdx.x + h]);
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) p.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 6 + threadIdx.x] = sm[threadIdx.x][0];
+}
+
+// part[n][6] (min, max, min, max, min, max) -> part2[gridDim.x][6]
+__global__ __launch_bounds__(kThreads) void k_minmax6(const double* part, long long n, double* part2) {
+  __shared__ double sm[6][kThreads];
+  double v[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
+  for (long long b = (long long)blockIdx.x * kThreads + threadIdx.x; b < n; b += (long long)gridDim.x * kThreads)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v[c] = (c & 1) ? fmax(v[c], part[b * 6 + c]) : fmin(v[c], part[b * 6 + c]);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) sm[c][threadIdx.x] = v[c];
+  __syncthreads();
+  for (int h = kThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        sm[c][threadIdx.x] = (c & 1) ? fmax(sm[c][threadIdx.x], sm[c][threadIdx.x + h])
+                                     : fmin(sm[c][threadIdx.x], sm[c][threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part2[(size_t)blockIdx.x * 6 + threadIdx.x] = sm[threadIdx.x][0];
+}
+
 // ---- evaluation ------------------------------------------------------------
 constexpr int kMinmaxPer = 8;  // loads in flight per thread per iteration
 
@@ -381,6 +494,68 @@ int mr_combine_device(mr_ctx* ctx, int kind, double param, uint64_t seed, int64_
     if (v.out_dtype == MR_OUT_F64) hipLaunchKernelGGL(k_combine<double>, grid, dim3(kThreads), 0, st, q);
     else hipLaunchKernelGGL(k_combine<float>, grid, dim3(kThreads), 0, st, q);
     MR_HIP(hipGetLastError());
+  }
+  MR_HIP(hipStreamSynchronize(st));
+  return MR_OK;
+}
+
+int mr_combine_all_device(mr_ctx* ctx, double alpha, double ibm_percentage, double ibm_probability, uint64_t seed,
+                          int64_t pair_base, int64_t n_pairs, const void* ubm, const void* ibm, void* out_linear,
+                          void* out_aggregation, void* out_stochastic, double* minmax) {
+  if (!ctx || !ubm || !ibm || !out_linear || !out_aggregation || !out_stochastic)
+    return fail(MR_E_INVALID, "null argument");
+  // MR:366-369 / MR:434-437: the reference prints and calls System.exit(-1)
+  if (!(ibm_percentage >= 0.0 && ibm_percentage <= 1.0) || !(ibm_probability >= 0.0 && ibm_probability <= 1.0))
+    return fail(MR_E_INVALID, "percentage %g / probability %g must be between 0 and 1", ibm_percentage,
+                ibm_probability);
+  mr_view v;
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  if (pair_base < 0 || n_pairs < 0) return fail(MR_E_INVALID, "negative pair_base / n_pairs");
+  MR_HIP(hipSetDevice(v.device));
+  const int width = v.song_hi - v.song_lo;
+  const size_t esz = v.out_dtype == MR_OUT_F64 ? 8 : 4;
+  Comb3Params cp{v.n_test_users, width, v.song_lo, v.n_songs, alpha, ibm_probability, (unsigned long long)seed,
+                 (long long)pair_base, (long long)(ibm_percentage * (double)n_pairs),  // (p * length).toInt, MR:371
+                 reinterpret_cast<const long long*>(v.te_off), v.te_songs, ubm, ibm,
+                 {out_linear, out_aggregation, out_stochastic}, nullptr};
+  hipStream_t st = (hipStream_t)v.stream;
+  const int gx = (width + kThreads * kCombPer - 1) / (kThreads * kCombPer);
+  const long long nblk = (long long)gx * v.n_test_users;
+  Tmp<double> part, part2;
+  part.st = part2.st = st;
+  constexpr int kRed = 256;  // k_minmax6 blocks
+  if (minmax && nblk > 0) {
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&part.p), (size_t)nblk * 6 * sizeof(double), st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&part2.p), (size_t)kRed * 6 * sizeof(double), st));
+  }
+  for (int y0 = 0; gx > 0 && y0 < v.n_test_users; y0 += 65535) {
+    Comb3Params q = cp;
+    const int ny = std::min(65535, v.n_test_users - y0);
+    q.n_te = ny;
+    q.te_off = cp.te_off + y0;  // values index the whole te_songs (see mr_combine_device)
+    q.pair_base = cp.pair_base + (long long)y0 * v.n_songs;
+    q.ubm = (const char*)ubm + (size_t)y0 * width * esz;
+    q.ibm = (const char*)ibm + (size_t)y0 * width * esz;
+    for (int c = 0; c < 3; ++c) q.out[c] = (char*)cp.out[c] + (size_t)y0 * width * esz;
+    q.part = part.p ? part.p + (size_t)y0 * gx * 6 : nullptr;
+    dim3 grid(gx, ny);
+    if (v.out_dtype == MR_OUT_F64) hipLaunchKernelGGL(k_combine3<double>, grid, dim3(kThreads), 0, st, q);
+    else hipLaunchKernelGGL(k_combine3<float>, grid, dim3(kThreads), 0, st, q);
+    MR_HIP(hipGetLastError());
+  }
+  if (minmax) {
+    double h[kRed * 6];
+    for (int c = 0; c < 6; ++c) minmax[c] = (c & 1) ? -INFINITY : INFINITY;
+    if (nblk > 0) {
+      hipLaunchKernelGGL(k_minmax6, dim3(kRed), dim3(kThreads), 0, st, part.p, nblk, part2.p);
+      MR_HIP(hipGetLastError());
+      MR_HIP(hipMemcpyAsync(h, part2.p, sizeof h, hipMemcpyDeviceToHost, st));
+      MR_HIP(hipStreamSynchronize(st));
+      for (int b = 0; b < kRed; ++b)
+        for (int c = 0; c < 6; ++c)
+          minmax[c] = (c & 1) ? std::fmax(minmax[c], h[b * 6 + c]) : std::fmin(minmax[c], h[b * 6 + c]);
+    }
   }
   MR_HIP(hipStreamSynchronize(st));
   return MR_OK;

@@ -219,6 +219,20 @@ class Engine:
                                              int(n_pairs), ctypes.c_void_p(ubm_ptr), ctypes.c_void_p(ibm_ptr),
                                              ctypes.c_void_p(out_ptr)), "mr_combine_device")
 
+    def combine_all(self, alpha: float, ibm_percentage: float, ibm_probability: float, ubm_ptr: int, ibm_ptr: int,
+                    out_ptrs: Tuple[int, int, int], *, seed: int = 0, pair_base: int = 0,
+                    n_pairs: int = 0) -> Tuple[Tuple[float, float], Tuple[float, float], Tuple[float, float]]:
+        """The linear, aggregation and stochastic combinations in one pass
+        (mr_combine_all_device), each bit-equal to combine(); returns each
+        output's (min, max) over its pairs; synchronous."""
+        mm = (ctypes.c_double * 6)()
+        _lib.check(self._L.mr_combine_all_device(self._h, float(alpha), float(ibm_percentage), float(ibm_probability),
+                                                 int(seed) & (2 ** 64 - 1), int(pair_base), int(n_pairs),
+                                                 ctypes.c_void_p(ubm_ptr), ctypes.c_void_p(ibm_ptr),
+                                                 *(ctypes.c_void_p(x) for x in out_ptrs), mm),
+                   "mr_combine_all_device")
+        return (mm[0], mm[1]), (mm[2], mm[3]), (mm[4], mm[5])
+
     def eval_minmax(self, dense_ptr: int) -> Tuple[float, float]:
         mn, mx = ctypes.c_double(), ctypes.c_double()
         _lib.check(self._L.mr_eval_minmax_device(self._h, ctypes.c_void_p(dense_ptr), ctypes.byref(mn),

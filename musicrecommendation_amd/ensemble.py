@@ -125,6 +125,28 @@ class DeviceEnsemble:
         """getStochasticCombinationModel (MR:429-481), seeded."""
         return self._combine(STOCHASTIC, ubm, ibm, item_based_probability, seed)
 
+    def combinations(self, ubm, ibm, alpha: float = 0.5, item_based_percentage: float = 0.5,
+                     item_based_probability: float = 0.5, seed: int = 0):
+        """The driver's three combinations (main.scala:57-89: linear, aggregation,
+        stochastic) in one pass over ubm and ibm (mr_combine_all_device), each
+        bit-equal to linear() / aggregation() / stochastic(). Each output keeps
+        its min / max from the same pass for threshold_map, valid while the
+        tensor is unmodified (torch's version counter)."""
+        outs = (self.empty(), self.empty(), self.empty())
+        self._after_torch()
+        mms = self.e.combine_all(alpha, item_based_percentage, item_based_probability, ubm.data_ptr(),
+                                 ibm.data_ptr(), tuple(t.data_ptr() for t in outs), seed=seed,
+                                 pair_base=self.pair_base, n_pairs=self.n_pairs)
+        for t, mm in zip(outs, mms):
+            t._mr_minmax = (t._version, mm[0], mm[1])
+        return outs
+
+    def _minmax(self, t) -> Tuple[float, float]:
+        cached = getattr(t, "_mr_minmax", None)
+        if cached is not None and cached[0] == t._version:  # from the producing pass, tensor unchanged
+            return cached[1], cached[2]
+        return self.e.eval_minmax(t.data_ptr())
+
     # ---- evaluation --------------------------------------------------------------
     def _world(self) -> int:
         import torch.distributed as dist
@@ -138,7 +160,7 @@ class DeviceEnsemble:
         import torch.distributed as dist
 
         self._after_torch()
-        mn, mx = self.e.eval_minmax(t.data_ptr())
+        mn, mx = self._minmax(t)
         world = self._world()
         if world > 1:
             be = dist.get_backend(self.group)

@@ -81,6 +81,35 @@ def test_combinations_and_map_bit_identical(dtype):
                 ens.aggregation(ubm_t, ibm_t, 1.2)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_combinations_in_one_pass(dtype):
+    """mr_combine_all_device: the three outputs bitwise equal to the separate
+    calls, their min / max equal to mr_eval_minmax_device, the mAP through the
+    carried min / max equal to the recomputed one; a block of test users and
+    a song shard too; an in-place edit drops the carried min / max."""
+    ds = synth.config("c2", n_test=24).dataset()
+    n_pairs = ds.n_pairs()
+    for song_lo, song_hi, a, b in [(0, ds.n_songs, 0, ds.n_test), (0, ds.n_songs, 7, 19), (3000, 9000, 0, ds.n_test)]:
+        sub = ds if (a, b) == (0, ds.n_test) else ds.subset_test_users(a, b)
+        base = a * ds.n_songs - int(ds.te_off[a])
+        with Engine(sub, out_dtype=dtype, song_lo=song_lo, song_hi=song_hi) as e:
+            ens = DeviceEnsemble(e, pair_base=base, n_pairs=n_pairs, pos=evaluation.label_pos(ds),
+                                 n_label_songs=ds.n_label_songs)
+            u_t, i_t = ens.model("ubm"), ens.model("ibm")
+            lin, agg, sto = ens.combinations(u_t, i_t, 0.3, 0.37, 0.5, seed=5)
+            sep = (ens.linear(u_t, i_t, 0.3), ens.aggregation(u_t, i_t, 0.37), ens.stochastic(u_t, i_t, 0.5, seed=5))
+            for got, exp in zip((lin, agg, sto), sep):
+                assert np.array_equal(got.cpu().numpy(), exp.cpu().numpy(), equal_nan=True)
+                assert got._mr_minmax[1:] == e.eval_minmax(got.data_ptr())
+            if (song_lo, song_hi, a, b) == (0, ds.n_songs, 0, ds.n_test):
+                for got, exp in zip((lin, agg, sto), sep):
+                    assert ens.threshold_map(got) == ens.threshold_map(exp)
+                lin.mul_(2.0)  # in place: the carried min / max no longer apply
+                assert ens._minmax(lin) == e.eval_minmax(lin.data_ptr())
+                with pytest.raises(_lib.EngineError):
+                    ens.combinations(u_t, i_t, 0.5, 1.5, 0.5)
+
+
 def test_map_vs_literal_fixture():
     for name in ("tiny", "small"):
         ds, z = synth_fixture(name)
