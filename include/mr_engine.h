@@ -348,6 +348,11 @@ int mr_combine_all_device(mr_ctx* ctx, double alpha, double ibm_percentage, doub
 /* evaluateModel (MR:636), device part: min / max over the model's scores
  * (MR:524-525; +inf / -inf when the shard holds no pair) ... */
 int mr_eval_minmax_device(mr_ctx* ctx, const void* dense, double* mn, double* mx);
+/* The same min / max for the dense model of the context's last mr_run /
+ * mr_run_into, computed by the wide-shape scoring kernels while they store it
+ * (per-user ordered-key atomics; no second pass over the model). MR_E_STATE
+ * when the last run was not a wide-shape dense run (or was a graph replay). */
+int mr_dense_minmax(mr_ctx* ctx, double* mn, double* mx);
 /* ... and per song s of the shard and threshold t_i = i/10, i < n_thresholds:
  * pred_counts[s][i] = #test users with (x - mn)/(mx - mn) > t_i (MR:529),
  * tp_counts[s][i] = those of them whose labels hold s (MR:545). n_thresholds:

@@ -170,6 +170,7 @@ SIGNATURES = {
     "mr_combine_all_device": (c_int, [c_void_p, c_double, c_double, c_double, ctypes.c_uint64, c_int64, c_int64,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, POINTER(c_double)]),
     "mr_eval_minmax_device": (c_int, [c_void_p, c_void_p, POINTER(c_double), POINTER(c_double)]),
+    "mr_dense_minmax": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
     "mr_eval_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_int32]),
     "mr_eval_map_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_int32,

@@ -228,6 +228,20 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // no LDS round trip, unlike __shfl's ds_bpermute). Every lane must be active.
 __device__ __forceinline__ int wave_lane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
+// Doubles as unsigned keys in the same order (negatives: bits inverted;
+// others: sign bit set), so integer atomicMin / atomicMax give min / max.
+__host__ __device__ inline unsigned long long ordered_key(double x) {
+  unsigned long long b;
+  memcpy(&b, &x, sizeof b);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__host__ __device__ inline double ordered_value(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  double x;
+  memcpy(&x, &b, sizeof x);
+  return x;
+}
+
 // Block-wide exclusive scan of one int per thread (256 threads). `sbuf` holds kWaves ints.
 __device__ __forceinline__ int block_excl_scan(int x, int* total, int* sbuf) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1039,6 +1053,10 @@ struct ScoreParams {
   const long long* seg_off;      // [tile][row]: first pool entry of the row's tile segment
   const int* seg_len;            // [tile][row]: its entries
   const unsigned* pool;          // entries (tile-local song << kCoocCntBits) | C[s2][s]
+  // wide shape, dense output: ordered keys of each user's min / max stored
+  // score ([user] min, [mm_n + user] max; mr_dense_minmax), or null
+  unsigned long long* mm_key;
+  int mm_n;
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -1993,6 +2011,15 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   OutT* out = reinterpret_cast<OutT*>(p.dense_out) + (size_t)u * p.width + (blo - p.song_lo);
   long long mk = kKeyNone;
   int ms = INT_MAX;
+  OutT lmn = (OutT)INFINITY, lmx = (OutT)-INFINITY;  // stored scores' min / max (p.mm_key)
+  auto store = [&](int i, bool h, double score) {
+    const OutT o = h ? (OutT)NAN : (OutT)score;
+    out[i] = o;
+    if (!h) {
+      lmn = o < lmn ? o : lmn;
+      lmx = o > lmx ? o : lmx;
+    }
+  };
   constexpr int EB = MR_WIDE_EB;
   int i_start = tid;
   if constexpr (kPF) {  // the prefetched songs first
@@ -2003,7 +2030,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
       double score = (double)(long long)acc[i] * inv_f;
       score = score / scp[e];
-      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      if (p.dense) store(i, h, score);
       const long long key = h ? kKeyNone : __double_as_longlong(score);
       acc[i] = (unsigned long long)key;
       if (key >= 0) take_if_before(mk, ms, key, blo + i);
@@ -2030,10 +2057,22 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       const bool h = (heard[i >> 5] >> (i & 31)) & 1u;
       double score = (double)(long long)av[e] * inv_f;
       if (MODEL == MR_IBM) score = score / sc[e];
-      if (p.dense) out[i] = h ? (OutT)NAN : (OutT)score;
+      if (p.dense) store(i, h, score);
       const long long key = h ? kKeyNone : __double_as_longlong(score);
       acc[i] = (unsigned long long)key;
       if (key >= 0) take_if_before(mk, ms, key, blo + i);
+    }
+  }
+  if (p.mm_key) {  // the wave's min / max, one atomic each per wave (ordered keys)
+    double a = (double)lmn, b = (double)lmx;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a = fmin(a, __shfl_xor(a, o, 64));
+      b = fmax(b, __shfl_xor(b, o, 64));
+    }
+    if (lane == 0) {
+      atomicMin(&p.mm_key[u], ordered_key(a));
+      atomicMax(&p.mm_key[p.mm_n + u], ordered_key(b));
     }
   }
   const int k = KS == 10 ? 10 : p.topk;
@@ -3349,6 +3388,8 @@ struct mr_ctx {
   bool win_open = false;
   bool win_stopped = false;  // mr_timing_stop recorded win[1]
   void* dense_override = nullptr;  // mr_run_into: caller's device buffer for this run's dense model
+  DevBuf<unsigned long long> mm_key;  // wide dense runs: per-user min / max keys of the stored scores
+  bool mm_on = false, mm_valid = false;
   hipGraph_t graph = nullptr;          // mr_graph_capture: n steps of mr_run
   hipGraphExec_t graph_exec = nullptr;
   int graph_steps = 0;
@@ -3398,6 +3439,7 @@ struct mr_ctx {
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
     dense.release();
+    mm_key.release(); mm_on = mm_valid = false;
     stamps.release();
     flag.release();
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
@@ -4691,6 +4733,7 @@ int run_cooc(mr_ctx* c) {
     sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
     sp.stamps = y0 == 0 ? c->stamps.p : nullptr;  // diagnostic build: the first launch
     sp.topk_lists = c->opt.topk_lists;
+    if (c->mm_on) { sp.mm_key = c->mm_key.p; sp.mm_n = c->n_te; }
     hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(c->cooc_nt), c->cooc_score_lds, st, sp);
     MR_HIP(hipGetLastError());
     if (k > 0 && c->n_tiles > 1) {
@@ -4777,6 +4820,7 @@ int run_model(mr_ctx* c, int model) {
       sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       sp.topk_lists = c->opt.topk_lists;
+      if (c->mm_on && wide) { sp.mm_key = c->mm_key.p; sp.mm_n = c->n_te; }
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
                          c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
@@ -4940,15 +4984,47 @@ int mr_run(mr_ctx* c, int model) {
   if (!c->loaded) return fail(MR_E_STATE, "mr_run before mr_load");
   if (model != MR_UBM && model != MR_IBM) return fail(MR_E_INVALID, "unknown model %d", model);
   MR_HIP(hipSetDevice(c->opt.device));
+  // wide dense runs leave each user's min / max stored score (mr_dense_minmax)
+  c->mm_valid = false;
+  c->mm_on = c->shape == kShapeWide && c->opt.dense && c->n_te > 0;
+  if (c->mm_on) {
+    int rc0 = MR_OK;
+    if (!c->mm_key.p && (rc0 = dev_alloc(c->mm_key, (size_t)2 * c->n_te))) return rc0;
+    MR_HIP(hipMemsetAsync(c->mm_key.p, 0xff, (size_t)c->n_te * 8, c->stream));  // min keys: the largest
+    MR_HIP(hipMemsetAsync(c->mm_key.p + c->n_te, 0, (size_t)c->n_te * 8, c->stream));  // max keys: the smallest
+  }
   int rc = run_model(c, model);
+  const bool mm = c->mm_on;
+  c->mm_on = false;
   if (rc) return rc;
+  c->mm_valid = mm;
   c->ran = true;
   c->last_model = model;
   return MR_OK;
 }
 
+int mr_dense_minmax(mr_ctx* c, double* mn, double* mx) {
+  if (!c || !mn || !mx) return fail(MR_E_INVALID, "null argument");
+  if (!c->mm_valid)
+    return fail(MR_E_STATE, "no dense min / max: the last mr_run / mr_run_into was not a wide-shape dense run");
+  MR_HIP(hipSetDevice(c->opt.device));
+  std::vector<unsigned long long> h((size_t)2 * c->n_te);
+  MR_HIP(hipMemcpyAsync(h.data(), c->mm_key.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  MR_HIP(hipStreamSynchronize(c->stream));
+  unsigned long long a = ~0ull, b = 0ull;
+  for (int u = 0; u < c->n_te; ++u) {
+    a = std::min(a, h[u]);
+    b = std::max(b, h[(size_t)c->n_te + u]);
+  }
+  // (no pair anywhere: +inf / -inf, as mr_eval_minmax_device)
+  *mn = a == ~0ull ? INFINITY : ordered_value(a);
+  *mx = b == 0ull ? -INFINITY : ordered_value(b);
+  return MR_OK;
+}
+
 int mr_graph_capture(mr_ctx* c, int model, int32_t n_steps) {
   if (!c) return fail(MR_E_INVALID, "null context");
+  c->mm_valid = false;
   if (!c->loaded) return fail(MR_E_STATE, "mr_graph_capture before mr_load");
   if (model != MR_UBM && model != MR_IBM) return fail(MR_E_INVALID, "unknown model %d", model);
   if (n_steps < 1 || n_steps > 100000) return fail(MR_E_INVALID, "n_steps %d outside [1,100000]", n_steps);
@@ -4975,6 +5051,7 @@ int mr_graph_capture(mr_ctx* c, int model, int32_t n_steps) {
 }
 
 int mr_graph_launch(mr_ctx* c) {
+  if (c) c->mm_valid = false;  // (graph replays leave no dense min / max)
   if (!c) return fail(MR_E_INVALID, "null context");
   if (!c->graph_exec) return fail(MR_E_STATE, "no captured graph (mr_graph_capture)");
   MR_HIP(hipSetDevice(c->opt.device));

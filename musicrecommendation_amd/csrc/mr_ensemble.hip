@@ -76,7 +76,10 @@ __host__ __device__ inline float pair_uniform(unsigned long long seed, long long
   return (float)(unsigned)(z >> 40) * (1.0f / 16777216.0f);
 }
 
-constexpr int kCombPer = 4;  // songs per thread (strided by kThreads: coalesced)
+#ifndef MR_COMB_PER
+#define MR_COMB_PER 8  // C5: 86.44 vs 87.00 ms per step at 4 (profiles/r04/s35)
+#endif
+constexpr int kCombPer = MR_COMB_PER;  // songs per thread (strided by kThreads: coalesced)
 
 // One (user, kThreads * kCombPer-song block) per workgroup. The pair index
 // needs |{t in T(u): t < s}|: one binary search per block for the first heard
@@ -325,6 +328,9 @@ __device__ __forceinline__ int levels(double x, double mn, double mx, int n_thr)
 }
 
 // one thread per song column, a block of users per blockIdx.y (rows read coalesced)
+#ifndef MR_EVAL_U
+#define MR_EVAL_U 16  // C5: 86.53 vs 87.00 ms per step at 8 (profiles/r04/s35)
+#endif
 template <typename OutT>
 __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   const int i = blockIdx.x * kThreads + threadIdx.x;
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
   int cnt[kThresholds];
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t) cnt[t] = 0;
-  constexpr int U = 8;  // rows in flight per thread
+  constexpr int U = MR_EVAL_U;  // rows in flight per thread
   for (int ub = u0; ub < u1; ub += U) {
     OutT x[U];
 #pragma unroll

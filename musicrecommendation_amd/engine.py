@@ -233,6 +233,14 @@ class Engine:
                    "mr_combine_all_device")
         return (mm[0], mm[1]), (mm[2], mm[3]), (mm[4], mm[5])
 
+    def dense_minmax(self) -> Optional[Tuple[float, float]]:
+        """(min, max) of the last run's dense model from the scoring kernels
+        (mr_dense_minmax), or None when the last run did not compute it."""
+        mn, mx = ctypes.c_double(), ctypes.c_double()
+        if self._L.mr_dense_minmax(self._h, ctypes.byref(mn), ctypes.byref(mx)) != 0:
+            return None
+        return mn.value, mx.value
+
     def eval_minmax(self, dense_ptr: int) -> Tuple[float, float]:
         mn, mx = ctypes.c_double(), ctypes.c_double()
         _lib.check(self._L.mr_eval_minmax_device(self._h, ctypes.c_void_p(dense_ptr), ctypes.byref(mn),

@@ -104,6 +104,9 @@ class DeviceEnsemble:
         self._after_torch()
         self.e.run_into(name, t.data_ptr())
         self.e.sync()
+        mm = self.e.dense_minmax()  # the scoring kernels' min / max (wide shape), for threshold_map
+        if mm is not None:
+            t._mr_minmax = (t._version, mm[0], mm[1])
         return t
 
     def _combine(self, kind: int, ubm, ibm, param: float, seed: int = 0):

@@ -110,6 +110,34 @@ def test_combinations_in_one_pass(dtype):
                     ens.combinations(u_t, i_t, 0.5, 1.5, 0.5)
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+@pytest.mark.parametrize("route", ["two_hop", "cooc"])
+def test_dense_minmax_from_the_scoring_kernels(dtype, route):
+    """mr_dense_minmax (wide shape: min / max kept by the scoring kernels while
+    they store the model) equals mr_eval_minmax_device over the stored model,
+    for both models and both ibm routes, over a song shard and user batches;
+    threshold_map through it equals the recomputed one; a fused-shape run
+    and a top-k-only context leave none."""
+    ds = synth.config("c2", n_test=24).dataset()
+    for lo, hi in [(0, ds.n_songs), (2000, 11000)]:
+        with Engine(ds, out_dtype=dtype, stage1="wide", song_lo=lo, song_hi=hi, ibm_route=route) as e:
+            ens = DeviceEnsemble(e)
+            for model in ("ubm", "ibm"):
+                t = ens.model(model)
+                mm = e.dense_minmax()
+                assert mm is not None and mm == e.eval_minmax(t.data_ptr()), (model, lo)
+                assert t._mr_minmax[1:] == mm
+                if (lo, hi) == (0, ds.n_songs):
+                    host = evaluation.threshold_map(t.cpu().numpy().astype(np.float64), ds)
+                    assert ens.threshold_map(t) == host
+    with Engine(ds, out_dtype=dtype, stage1="fused") as e:
+        e.run("ibm")
+        assert e.dense_minmax() is None
+    with Engine(ds, out_dtype=dtype, stage1="wide", dense=False) as e:
+        e.run("ubm")
+        assert e.dense_minmax() is None
+
+
 def test_map_vs_literal_fixture():
     for name in ("tiny", "small"):
         ds, z = synth_fixture(name)
