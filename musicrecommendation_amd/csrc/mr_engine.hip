@@ -4070,7 +4070,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   trace("tiles");
   // Separate / wide shapes: test-user batches so the neighbour lists fit 8 GiB.
   const int cap = n_chunks * chunk;
-  const size_t budget = (size_t)8 << 30;
+  // one launch's neighbour lists (batch x cap x 12 B): an eighth of the free
+  // device memory, 8-32 GiB (C5's 2,000 users in one launch on a 288 GB
+  // MI355X; allocated at the first two-hop run, ensure_nbr)
+  size_t free_b0 = 0, total_b0 = 0;
+  MR_HIP(hipMemGetInfo(&free_b0, &total_b0));
+  const size_t budget = std::min<size_t>((size_t)32 << 30, std::max<size_t>((size_t)8 << 30, free_b0 / 8));
   const int batch = fused ? n_te
                           : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
                                                                       budget / ((size_t)cap * 12)));
@@ -4299,11 +4304,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     }
     if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
     if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
-  } else {
-    if ((rc = dev_alloc(c->nbr_v, (size_t)batch * cap))) return rc;
-    if ((rc = dev_alloc(c->nbr_q, (size_t)batch * cap))) return rc;
-    if ((rc = dev_alloc(c->nbr_cnt, (size_t)batch * n_chunks))) return rc;
-  }
+  }  // (separate / wide shapes: neighbour lists allocated by the first two-hop run, ensure_nbr)
   if (route == 2) {
     const size_t nr = row_song.size();
     if ((rc = dev_upload(c->row_song, row_song.data(), nr, st))) return rc;
@@ -4749,6 +4750,19 @@ int run_cooc(mr_ctx* c) {
   return MR_OK;
 }
 
+// The two-hop shapes' neighbour lists (batch x cap entries), allocated when a
+// two-hop run first needs them: a context that only runs the co-listening
+// route (C4's north star) never holds them. Not during graph capture
+// (mr_graph_capture calls this first).
+int ensure_nbr(mr_ctx* c) {
+  if (c->shape == kShapeFused || (c->nbr_v.p && c->nbr_q.p && c->nbr_cnt.p)) return MR_OK;
+  int rc;
+  if ((rc = dev_alloc(c->nbr_v, (size_t)c->batch * c->cap))) return rc;
+  if ((rc = dev_alloc(c->nbr_q, (size_t)c->batch * c->cap))) return rc;
+  if ((rc = dev_alloc(c->nbr_cnt, (size_t)c->batch * c->n_chunks))) return rc;
+  return MR_OK;
+}
+
 int run_model(mr_ctx* c, int model) {
   if (model == MR_IBM && c->ibm_route == 2) {
     c->cooc_ran = true;
@@ -4771,7 +4785,9 @@ int run_model(mr_ctx* c, int model) {
       MR_HIP(hipEventRecord(ev[0], st));
     }
     if (c->shape == kShapeSeparate || c->shape == kShapeWide) {
-      if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) return fail(MR_E_STATE, "separate shape without neighbour buffers");
+      if (!c->nbr_v.p || !c->nbr_q.p || !c->nbr_cnt.p) {
+        if (int rc0 = ensure_nbr(c)) return rc0;
+      }
       NbrParams np{c->n_tr, user0, c->cap, c->opt.frac_bits, c->chunk, c->n_chunks, c->te_off.p, c->te_songs.p,
                    c->trs_off.p, c->trs_users.p, c->q_song.p, c->sqrt_tr.p, c->sqrt_te.p, c->nbr_v.p, c->nbr_q.p,
                    c->nbr_cnt.p, c->n_chunks > 1 ? c->sbound.p : nullptr};
@@ -5031,6 +5047,9 @@ int mr_graph_capture(mr_ctx* c, int model, int32_t n_steps) {
   if (c->opt.time_kernels) return fail(MR_E_STATE, "graph capture of a context with time_kernels=1");
   MR_HIP(hipSetDevice(c->opt.device));
   MR_HIP(hipStreamSynchronize(c->stream));
+  if (!(model == MR_IBM && c->ibm_route == 2)) {  // no allocation inside the capture
+    if (int rc0 = ensure_nbr(c)) return rc0;
+  }
   if (c->graph_exec) { MR_HIP(hipGraphExecDestroy(c->graph_exec)); c->graph_exec = nullptr; }
   if (c->graph) { MR_HIP(hipGraphDestroy(c->graph)); c->graph = nullptr; }
   c->graph_steps = 0;
