@@ -182,3 +182,27 @@ def test_gloo_world2_threshold_map_reduction(layout, n_thr):
     ref = evaluation.threshold_map(z["ibm"], ds,
                                    evaluation.THRESHOLDS if n_thr == 10 else evaluation.THRESHOLDS_DISTRIBUTED)
     assert all(res[r] == ref for r in range(world))
+
+
+def test_carried_minmax_follows_the_tensor_version():
+    """DeviceEnsemble._minmax: a min / max carried from the producing pass
+    (combinations(), model() on the wide shape) is used while the tensor is
+    unmodified, and recomputed (mr_eval_minmax_device) after an in-place edit
+    or when none was carried."""
+    import torch
+
+    class FakeEngine:
+        calls = 0
+
+        def eval_minmax(self, ptr):
+            FakeEngine.calls += 1
+            return (-1.0, 1.0)
+
+    ens = DeviceEnsemble.__new__(DeviceEnsemble)
+    ens.e = FakeEngine()
+    t = torch.zeros(4)
+    assert ens._minmax(t) == (-1.0, 1.0) and FakeEngine.calls == 1  # nothing carried
+    t._mr_minmax = (t._version, 0.25, 0.5)
+    assert ens._minmax(t) == (0.25, 0.5) and FakeEngine.calls == 1  # carried, unchanged
+    t.add_(1.0)
+    assert ens._minmax(t) == (-1.0, 1.0) and FakeEngine.calls == 2  # edited in place
