@@ -228,19 +228,6 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 // no LDS round trip, unlike __shfl's ds_bpermute). Every lane must be active.
 __device__ __forceinline__ int wave_lane(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
 
-// Light rows' emission over a shard of at most kLightFewTiles tiles (C4 over 8
-// GPUs: 3): per-tile counts and cursors advanced once per wave and tile
-// (ballot + popcount + v_mbcnt), not once per entry — the per-entry LDS
-// atomics all hit the same 3 words. MR_LIGHT_FEW=0: per entry (A/B).
-#ifndef MR_LIGHT_FEW
-#define MR_LIGHT_FEW 1
-#endif
-constexpr int kLightFewTiles = 4;
-// Lanes below this one whose bit is set in m (v_mbcnt).
-__device__ __forceinline__ int lanes_below(unsigned long long m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-
 // Doubles as unsigned keys in the same order (negatives: bits inverted;
 // others: sign bit set), so integer atomicMin / atomicMax give min / max.
 __host__ __device__ inline unsigned long long ordered_key(double x) {
@@ -2636,20 +2623,9 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   stamp_rt(sb, 2);
   // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
-  const bool few = MR_LIGHT_FEW && p.n_tiles <= kLightFewTiles;  // (uniform)
-  for (int i = tid; i < S; i += NT) {  // (S is a multiple of NT: every lane in every step)
+  for (int i = tid; i < S; i += NT) {
     const unsigned x = tab[i];
-    if (few) {  // a few tiles (narrow shards): one add per wave and tile, not per entry
-      const int t = x ? (int)((x >> kLightCntBits) - 1u) / bs : -1;
-#pragma unroll
-      for (int tt = 0; tt < kLightFewTiles; ++tt) {
-        if (tt >= p.n_tiles) break;
-        const unsigned long long m = __ballot(t == tt);
-        if ((tid & 63) == 0 && m) atomicAdd(&tcnt[tt], (int)__popcll(m));
-      }
-    } else if (x) {
-      atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
-    }
+    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
   }
   __syncthreads();
   stamp_rt(sb, 3);
@@ -2676,22 +2652,11 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   unsigned* out = p.pool + p.row_base[r];
   for (int i = tid; i < S; i += NT) {
     const unsigned x = tab[i];
-    const int key = x ? (int)((x >> kLightCntBits) - 1u) : 0;
-    const int t = x ? key / bs : -1;
-    const unsigned e = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
-    if (few) {  // a few tiles: the wave's entries of a tile at one cursor add
-#pragma unroll
-      for (int tt = 0; tt < kLightFewTiles; ++tt) {
-        if (tt >= p.n_tiles) break;
-        const unsigned long long m = __ballot(t == tt);
-        if (!m) continue;
-        int base = 0;
-        if ((tid & 63) == 0) base = atomicAdd(&tpos[tt], (int)__popcll(m));
-        base = wave_lane(base, 0);
-        if (t == tt) out[base + lanes_below(m)] = e;
-      }
-    } else if (x) {
-      out[atomicAdd(&tpos[t], 1)] = e;
+    if (x) {
+      const int key = (int)((x >> kLightCntBits) - 1u);
+      const int t = key / bs;
+      const int pos = atomicAdd(&tpos[t], 1);
+      out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
   }
   __syncthreads();
@@ -2735,20 +2700,9 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
   const int bs = p.block_songs;
-  const bool few = MR_LIGHT_FEW && p.n_tiles <= kLightFewTiles;  // (uniform)
   for (int i = lane; i < S; i += 64) {
     const unsigned x = tab[i];
-    if (few) {  // a few tiles: one add per tile and step
-      const int t = x ? (int)((x >> kLightCntBits) - 1u) / bs : -1;
-#pragma unroll
-      for (int tt = 0; tt < kLightFewTiles; ++tt) {
-        if (tt >= p.n_tiles) break;
-        const unsigned long long m = __ballot(t == tt);
-        if (lane == 0 && m) atomicAdd(&tcnt[tt], (int)__popcll(m));
-      }
-    } else if (x) {
-      atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
-    }
+    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
   }
   wave_lds_sync();
   {
@@ -2770,22 +2724,11 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   unsigned* out = p.pool + p.row_base[r];
   for (int i = lane; i < S; i += 64) {
     const unsigned x = tab[i];
-    const int key = x ? (int)((x >> kLightCntBits) - 1u) : 0;
-    const int t = x ? key / bs : -1;
-    const unsigned e = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
-    if (few) {  // a few tiles: one cursor add per tile and step
-#pragma unroll
-      for (int tt = 0; tt < kLightFewTiles; ++tt) {
-        if (tt >= p.n_tiles) break;
-        const unsigned long long m = __ballot(t == tt);
-        if (!m) continue;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&tpos[tt], (int)__popcll(m));
-        base = wave_lane(base, 0);
-        if (t == tt) out[base + lanes_below(m)] = e;
-      }
-    } else if (x) {
-      out[atomicAdd(&tpos[t], 1)] = e;
+    if (x) {
+      const int key = (int)((x >> kLightCntBits) - 1u);
+      const int t = key / bs;
+      const int pos = atomicAdd(&tpos[t], 1);
+      out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
   }
   wave_lds_sync();
