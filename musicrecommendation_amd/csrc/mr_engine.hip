@@ -1636,7 +1636,7 @@ constexpr int kCoocDenseTail = -3;
 __host__ __device__ inline int cooc_dense_words(int bw) { return ((bw + 3) / 4 + 3) & ~3; }
 constexpr int kCoocDenseDiv = 3;
 #ifndef MR_COOC_BIG_ROW
-#define MR_COOC_BIG_ROW 4096
+#define MR_COOC_BIG_ROW 2048  // C4 44.74 vs 45.16 ms at 4096, 8x1 6.06 vs 6.10 (profiles/r04/s43, s44)
 #endif
 constexpr int kCoocBigRow = MR_COOC_BIG_ROW;  // listeners from which a heavy row's tiles get a workgroup each  // dense when non-zeros * this >= the tile's songs (MR_COOC_DENSE_DIV)
 constexpr unsigned kCoocCntMask = (1u << kCoocCntBits) - 1u;
