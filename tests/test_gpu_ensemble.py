@@ -104,8 +104,10 @@ def test_combinations_in_one_pass(dtype):
             if (song_lo, song_hi, a, b) == (0, ds.n_songs, 0, ds.n_test):
                 for got, exp in zip((lin, agg, sto), sep):
                     assert ens.threshold_map(got) == ens.threshold_map(exp)
+                carried = lin._mr_minmax[1:]
                 lin.mul_(2.0)  # in place: the carried min / max no longer apply
-                assert ens._minmax(lin) == e.eval_minmax(lin.data_ptr())
+                torch.cuda.synchronize()  # (the engine's stream does not wait on torch's here)
+                assert ens._minmax(lin) == e.eval_minmax(lin.data_ptr()) != carried
                 with pytest.raises(_lib.EngineError):
                     ens.combinations(u_t, i_t, 0.5, 1.5, 0.5)
 
