@@ -2935,7 +2935,10 @@ __device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int 
 #ifndef MR_GROUP_PIPE
 #define MR_GROUP_PIPE 1
 #endif
-constexpr int kGroupPipeR = 4;
+#ifndef MR_GROUP_PIPE_R
+#define MR_GROUP_PIPE_R 4
+#endif
+constexpr int kGroupPipeR = MR_GROUP_PIPE_R;
 template <int NT>
 __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const int* lst, int n, int glog,
                                                      int width, unsigned* cnt, int* s_wcnt, int* s_tail,
