@@ -1584,6 +1584,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_WIDE_SEG
 #define MR_WIDE_SEG 12      // first entries of every segment loaded in one batch (wide kernel; swept 2-16)
 #endif
+#ifndef MR_WIDE_Z16
+#define MR_WIDE_Z16 1       // wide kernel: the accumulators zeroed by 16-B LDS stores
+#endif
 #ifndef MR_WIDE_EB
 #define MR_WIDE_EB 8        // wide-kernel epilogue: songs per thread whose scale loads are issued together
 #endif
@@ -1801,7 +1804,11 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       pf_s = p.te_songs[a + tid];
     }
   }
+#if MR_WIDE_Z16  // 16-B stores: two songs per store (acc is 16-B aligned; bs is even)
+  for (int i = tid; 2 * i < bw; i += NT) reinterpret_cast<ulonglong2*>(acc)[i] = make_ulonglong2(0ull, 0ull);
+#else
   for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
+#endif
   if constexpr (kDPF) {
     if (pf_r >= 0) {
       pf_sl = p.seg_len[(size_t)tile * p.n_rows + pf_r];
