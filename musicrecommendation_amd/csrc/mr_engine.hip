@@ -2618,7 +2618,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   const int S = rd.y & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);  // multiplicative hash: top log2(S) bits
-  for (int i = tid; i < S; i += NT) tab[i] = 0u;
+  for (int i = tid; 4 * i < S; i += NT) reinterpret_cast<uint4*>(tab)[i] = make_uint4(0u, 0u, 0u, 0u);  // (S: a power of 2 >= 1024)
   for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
   const int n = rd.w;
   const int* lst = p.trs_users + (unsigned)rd.z;
@@ -2696,7 +2696,7 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const int S = rd.y & kLightSlotsMask;
   const unsigned mask = (unsigned)S - 1u;
   const int sh = 32 - __builtin_ctz((unsigned)S);
-  for (int i = lane; i < S; i += 64) tab[i] = 0u;
+  for (int i = lane; 4 * i < S; i += 64) reinterpret_cast<uint4*>(tab)[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int i = lane; i < p.n_tiles; i += 64) { tcnt[i] = 0; tpos[i] = 0; }
   const int n = rd.w;
   const int* lst = p.trs_users + (unsigned)rd.z;
