@@ -2214,7 +2214,10 @@ constexpr int kLightSlotsMask = (1 << kLightGlogShift) - 1;
 // 4096 slots / 256 threads (7 per CU), 8192 / 512 (4), 16384 / 512 (2),
 // 32768 / 1024 (1). Tier 0 is the largest (launched first).
 constexpr int kLightTiers = 6;     // tiers 4, 5 (2048 / 1024 slots): one wave per row (k_cooc_light_wave)
-constexpr int kWaveRowsPerBlock = 4;
+#ifndef MR_WAVE_ROWS
+#define MR_WAVE_ROWS 4
+#endif
+constexpr int kWaveRowsPerBlock = MR_WAVE_ROWS;
 constexpr int kWaveMaxTiles = 64;  // the wave tiers' per-row tile counters
 __host__ __device__ constexpr int light_tier_slots(int t) { return 32768 >> t; }
 // a table of S slots holds a row whose entry bound is at most S * 4/5 (the
