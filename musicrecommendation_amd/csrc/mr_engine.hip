@@ -2215,7 +2215,7 @@ constexpr int kLightSlotsMask = (1 << kLightGlogShift) - 1;
 // 32768 / 1024 (1). Tier 0 is the largest (launched first).
 constexpr int kLightTiers = 6;     // tiers 4, 5 (2048 / 1024 slots): one wave per row (k_cooc_light_wave)
 #ifndef MR_WAVE_ROWS
-#define MR_WAVE_ROWS 4
+#define MR_WAVE_ROWS 1  // C4 8x1: 5.95 vs 6.03 ms at 4, 5.99 at 2 (profiles/r04/s54, s55)
 #endif
 constexpr int kWaveRowsPerBlock = MR_WAVE_ROWS;
 constexpr int kWaveMaxTiles = 64;  // the wave tiers' per-row tile counters
