@@ -54,6 +54,13 @@ README_C1_MS = {"ubm": 42857, "ibm": 70839}  # README.md:72 (sequential, 100/10)
 TEST_PER_GPU = 10
 
 
+def _pg() -> bool:
+    """A process group is up: N > 1 (torchrun), or the one-rank rehearsal of
+    the collective path (MR_BENCH_PG=1). Barriers and reductions run exactly
+    when this holds, so the one-rank rehearsal executes the N > 1 code."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def algorithmic_bytes(ds, out_bytes: int = 4, k: int = 10):
     """SURVEY.md §8d byte model, split per kernel.
     Per test user u with neighbours N(u) = ∪_{s2∈T(u)} L_tr(s2):
@@ -262,7 +269,8 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     ds = full if gu == 1 else full.subset_test_users(a, b)
     eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi, ibm_route=args.ibm_route)
     ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),
-                         pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs)
+                         pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs,
+                         collectives=True if _pg() else None)
     maps = {}
 
     def step():
@@ -278,7 +286,7 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     for _ in range(args.warmup):
         models = None  # release the previous step's buffers so the allocator reuses them
         models = step()
-    if world > 1:
+    if _pg():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -286,11 +294,11 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
         models = None
         models = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     t_max = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if _pg():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
     if rank == 0:
@@ -343,7 +351,7 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
             line["end_to_end"] = end_to_end_bulk(trip, "ibm")
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if _pg():
         dist.destroy_process_group()
 
 
@@ -410,7 +418,7 @@ def shared_bulk_dataset(cfg: str, world: int, rank: int):
     from musicrecommendation_amd.dataset import Dataset
 
     t0 = time.perf_counter()
-    if world == 1:
+    if not _pg():
         return synth.config(cfg).dataset(), time.perf_counter() - t0
     path = [None]
     full = None
@@ -458,17 +466,21 @@ def north_star(args, world: int, rank: int, local: int):
     timed region)."""
     from musicrecommendation_amd.sharding import ShardScorer
 
-    full, gen_s = shared_bulk_dataset("c4", world, rank)
+    cfg = args.ns_config
+    full, gen_s = shared_bulk_dataset(cfg, world, rank)
     gs = world
     t0 = time.perf_counter()
     scorer = ShardScorer(full, rank, world, local, song_groups=gs, topk=10, dense=False, out_dtype="f32",
                          ibm_route=args.ibm_route)
+    rehearse = _pg() and world == 1  # MR_BENCH_PG=1: the one-rank group runs the exchange too
+    scorer.exchange_always = rehearse
+    exchanging = scorer.gs > 1 or rehearse
     load_s = time.perf_counter() - t0
     free_b, total_b = torch.cuda.mem_get_info(scorer.device)
     eng = scorer.engine
 
     def timed(fn, k, window=False):
-        if world > 1:
+        if _pg():
             dist.barrier()
         torch.cuda.synchronize()
         scorer.sync()
@@ -481,10 +493,10 @@ def north_star(args, world: int, rank: int, local: int):
             eng.timing_stop()
         scorer.sync()
         torch.cuda.synchronize()
-        if world > 1:
+        if _pg():
             dist.barrier()
         el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device="cuda")
-        if world > 1:
+        if _pg():
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el.item())
 
@@ -492,16 +504,16 @@ def north_star(args, world: int, rank: int, local: int):
         scorer.step(args.model)
     step_s = timed(lambda: scorer.step(args.model), args.ns_steps, window=True)
     _n, win_ms = eng.timing_end()  # this rank's engine-stream time over the timed steps
-    exch_s = timed(scorer.exchange, args.ns_steps) if scorer.gs > 1 else 0.0
+    exch_s = timed(scorer.exchange, args.ns_steps) if exchanging else 0.0
     cooc = args.model == "ibm" and eng.ibm_route == "cooc"
     split = cooc_bytes(eng, scorer.ds, 0, 10) if cooc else {}
-    if cooc and scorer.gs > 1:  # the exchange's merge: G_s gathered lists read, one written, per user
+    if cooc and exchanging:  # the exchange's merge: G_s gathered lists read, one written, per user
         split["exchange_merge"] = 12 * 10 * scorer.ds.n_test * (scorer.gs + 1)  # this rank: G_s lists in, one out
     keys = ["build_heavy", "build_light", "score", "merge", "exchange_merge"]
     vec = [float(split.get(k_, 0)) for k_ in keys]
     vec += [float(scorer.pairs()), win_ms / args.ns_steps, host_peak_rss_gb(), float(total_b - free_b)]
     st = torch.tensor(vec, dtype=torch.float64, device="cuda")
-    if world > 1:
+    if _pg():
         sums = st.clone()
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         maxs = st.clone()
@@ -528,7 +540,7 @@ def north_star(args, world: int, rank: int, local: int):
                 if pmc.get("ibm_route") == "cooc" and pmc.get("layout", "1x1") == "1x1":
                     traffic = pmc.get("traffic_bytes_per_launch")
                     traffic_src = "profiles/pmc_c4.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, one C4 step)"
-            th = cached_twohop_bytes("c4", full)
+            th = cached_twohop_bytes(cfg, full)
             roof = {
                 "bound": "hbm", "kernel": "whole step: k_cooc_build + k_cooc_light* + k_score_wide<cooc> + "
                                           "k_topk_merge (+ the exchange's merge at N > 1)",
@@ -543,14 +555,14 @@ def north_star(args, world: int, rank: int, local: int):
                 "timing": "HIP events on each rank's engine stream around the timed steps; max over ranks",
                 "survey_two_hop": ({"bytes_per_step": th["total_bytes"], "source": "profiles/c4_twohop_bytes.json "
                                    "(scripts/twohop_bytes.py: SURVEY.md §8(d), top-10 only)",
-                                   "achieved_GBps": th["total_bytes"] / (dev_ms * 1e-3) / 1e9,
-                                   "frac": th["total_bytes"] / (dev_ms * 1e-3) / 1e9 / peak,
-                                   "note": "the survey's two-hop algorithm's bytes over the same time: the route "
-                                           "computes the same integer sums with fewer bytes (DESIGN.md §4b), so "
-                                           "this fraction may exceed 1"} if th else None),
+                                   "equivalent_GBps": th["total_bytes"] / (dev_ms * 1e-3) / 1e9,
+                                   "equivalent_frac": th["total_bytes"] / (dev_ms * 1e-3) / 1e9 / peak,
+                                   "note": "modelled, not measured: the survey's two-hop algorithm's bytes over "
+                                           "the same time; the route computes the same integer sums without "
+                                           "moving them (DESIGN.md §4b), so this may exceed 1"} if th else None),
             }
         out = {
-            "workload": f"c4: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} {full.n_train} train / "
+            "workload": f"{cfg}: {'ItemBasedModel' if args.model == 'ibm' else 'UserBasedModel'} {full.n_train} train / "
                         f"{full.n_test} test / {full.n_songs} songs, top-10 only",
             "layout": f"songs{scorer.gs}xusers{scorer.gu}", "song_shards": scorer.gs, "user_blocks": scorer.gu,
             "ibm_route": eng.ibm_route, "tiles_per_rank": eng.n_tiles, "block_songs": eng.block_songs,
@@ -559,15 +571,16 @@ def north_star(args, world: int, rank: int, local: int):
             "pairs_per_step": pairs, "steps": args.ns_steps, "warmup": args.ns_warmup,
             "ms_per_step": ms,  # slowest rank: max over ranks of the barrier-bracketed window
             "device_ms_per_step": dev_ms,
-            "exchange_ms_per_step": exch_s / args.ns_steps * 1e3 if scorer.gs > 1 else 0.0,
+            "exchange_ms_per_step": exch_s / args.ns_steps * 1e3 if exchanging else 0.0,
             "exchange": ("one all_gather_into_tensor of the top-k record blocks (int64 keys + int32 songs) per "
-                         "step inside each user block, then k_topk_merge on the device" if scorer.gs > 1 else
+                         "step inside each user block, then k_topk_merge on the device" if exchanging else
                          "none (one song shard: no exchange)"),
-            "allgather_bytes_per_rank": scorer.gs * scorer.rec_bytes if scorer.gs > 1 else 0,
+            "allgather_bytes_per_rank": scorer.gs * scorer.rec_bytes if exchanging else 0,
             "record_bytes": scorer.rec_bytes,
-            "process_group": {"backend": dist.get_backend() if world > 1 else None,
-                              "world_size": dist.get_world_size() if world > 1 else 1,
-                              "block_group_size": dist.get_world_size(scorer.group) if world > 1 else 1},
+            "process_group": {"backend": dist.get_backend() if _pg() else None,
+                              "world_size": dist.get_world_size() if _pg() else 1,
+                              "block_group_size": dist.get_world_size(scorer.group) if _pg() else 1,
+                              "rehearsal": "MR_BENCH_PG=1: one-rank group, exchange forced" if rehearse else None},
             "setup_s": {"dataset": gen_s, "shard_load": load_s},
             "host": {"threads_per_rank": _usable_threads(), "peak_rss_gb_max_rank": maxs[nk + 2],
                      "peak_rss_gb_sum": sums[nk + 2], "device_used_gb_after_load_max": maxs[nk + 3] / 2 ** 30},
@@ -646,6 +659,8 @@ def main() -> None:
                     help="skip the nested C4 2-D layout block (north_star) of the C2 line")
     ap.add_argument("--ns-steps", type=int, default=5, help="timed steps of the north_star block")
     ap.add_argument("--ns-warmup", type=int, default=2, help="warmup steps of the north_star block")
+    ap.add_argument("--ns-config", default="c4", help="dataset of the north_star block (c4; smaller ones for "
+                                                       "rehearsals of the collective path)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="independent C2 batches kept in flight per GPU (own context + stream each); "
                          "steps are issued round-robin, so up to this many overlap on the device")
@@ -675,12 +690,15 @@ def main() -> None:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     # Rehearsal overrides (never set by the driver): MR_BENCH_BACKEND=gloo and
     # MR_BENCH_DEVICE=0 let several ranks share one GPU to exercise the N > 1
-    # code paths on a one-GPU box. The real runs use RCCL, one GPU per rank.
+    # code paths on a one-GPU box; MR_BENCH_PG=1 brings the process group up at
+    # N = 1 too, so the driver's N > 1 collectives (RCCL init with device_id,
+    # broadcast_object_list, barriers, all-reduces, the all-gather exchange)
+    # run on one GPU. The real runs use RCCL, one GPU per rank.
     backend = os.environ.get("MR_BENCH_BACKEND", "nccl")
     if "MR_BENCH_DEVICE" in os.environ:
         local = int(os.environ["MR_BENCH_DEVICE"])
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or os.environ.get("MR_BENCH_PG") == "1":
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -727,7 +745,7 @@ def main() -> None:
         # fixed test set; small configs: weak, 10 test users per GPU in total.
         from musicrecommendation_amd.sharding import ShardScorer
 
-        if bulk and world > 1:  # built once on the node (rank 0), loaded by the other ranks
+        if bulk and _pg():  # built once on the node (rank 0), loaded by the other ranks
             trip = None
             full, _gen_s = shared_bulk_dataset(args.config, world, rank)
         else:
@@ -762,7 +780,7 @@ def main() -> None:
         eng.graph_capture(args.model, g_steps)
         eng.graph_launch()  # first replay uploads the graph: untimed
         drain()
-    if world > 1:
+    if _pg():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -780,7 +798,7 @@ def main() -> None:
     else:  # the closing event recorded, one device-wide wait (covers every stream)
         eng.timing_stop()
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if not args.stream_sync:
@@ -788,7 +806,7 @@ def main() -> None:
         drain()
     pairs_total_rank = rank_pairs(args.steps)  # pairs scored by this rank over the timed steps
     stats = torch.tensor([elapsed, pairs_total_rank], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if _pg():
         t_max = stats[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         tot = stats[1:].clone()
@@ -917,14 +935,14 @@ def main() -> None:
             line["cpu_baseline"] = None
         if world == 1 and not bulk and not args.no_e2e:
             line["end_to_end"] = end_to_end(ds, args.model)
-        if world == 1 and bulk and not args.no_e2e:
+        if world == 1 and bulk and not args.no_e2e and trip is not None:
             line["end_to_end"] = end_to_end_bulk(trip, args.model)
         if ns is not None:
             line["north_star"] = ns
         print(json.dumps(line), flush=True)
     for e in engines:
         e.close()
-    if world > 1:
+    if _pg():
         dist.destroy_process_group()
 
 

@@ -168,6 +168,16 @@ int mr_batch_info(const mr_ctx* ctx, int32_t* batch, int32_t* chunk, int32_t* n_
  * (a bound on the shard's non-zero counts; 4 B each). Any pointer may be NULL. */
 int mr_route_info(const mr_ctx* ctx, int32_t* route, int32_t* n_rows, int64_t* pool_entries);
 
+/* Tile top-k of the wide shape (the per-(test user, song tile) selection that
+ * feeds the segmented top-k merge, MR:249-257's scores ranked): *candidate_only
+ * = 1 when this context's top-k-only runs rank fp32 approximations of every
+ * song first and compute the exact fp64 score (the oracle's operations) of the
+ * candidates within a relative margin of the threshold only — lists, keys and
+ * scores bit-identical to the all-songs path; 0 when every song's exact score
+ * is computed (dense output, the fused / separate shapes, k > 64, or
+ * MR_WIDE_CAND=0 in the environment at mr_load). */
+int mr_topk_mode(const mr_ctx* ctx, int32_t* candidate_only);
+
 /* Sizes of the latest ibm run on the co-listening route (the byte model of
  * bench.py's roofline; synchronous): *index_nnz = non-zero counts C[s2][s]
  * over all index rows and the shard's songs, *consumed = Σ_u Σ_{s2 ∈ T(u)}

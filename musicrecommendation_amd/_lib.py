@@ -135,6 +135,7 @@ SIGNATURES = {
     "mr_launch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_batch_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "mr_route_info": (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int64)]),
+    "mr_topk_mode": (c_int, [c_void_p, POINTER(c_int32)]),
     "mr_cooc_stats": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "mr_cooc_bytes": (c_int, [c_void_p, POINTER(MrCoocBytes)]),
     "mr_shard_tile_songs": (c_int, [POINTER(MrOptions), c_int32, c_int32, POINTER(c_int32)]),

@@ -657,12 +657,14 @@ __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* c
 }
 
 
-// NG rows of NT / NG threads: more rows give a tighter tau (fewer survivors
-// to rank) for NG^2 / NT comparisons per thread.
-template <int NT, typename Get, int NG = NT / 16>
-__device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long long mk, int ms, unsigned char* gm,
-                                                     long long* ck, int* cs, int cap, long long* out_k, int* out_s,
-                                                     long long* sb = nullptr, const TopkDst& dst = TopkDst{}) {
+// The threshold of block_topk_threshold: every thread passes the best (mk,
+// ms) of its own entries; returns, uniformly, tau = the k-th best of the NG
+// row bests (k <= NG), or (0, INT_MAX) — "every valid key" — when fewer than
+// k rows hold a valid entry. Zeroes the scratch's survivor counter and ranks
+// (gm: topk_scratch_bytes(NT)); ends with a barrier.
+template <int NT, int NG = NT / 16>
+__device__ __forceinline__ void block_tau(int k, long long mk, int ms, unsigned char* gm, long long& tau_k,
+                                          int& tau_s, long long* sb = nullptr) {
   constexpr int GS = NT / NG;  // threads per row
   static_assert(NT % 64 == 0 && NT % NG == 0 && NG <= 64 && GS <= 64 && NT * 16 >= NG * NG,
                 "block shape");
@@ -672,7 +674,6 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   int* grank = counter + 1;                            // [NG]
   int* crank = grank + NG;                             // [256]
   const int tid = threadIdx.x, lane = tid & 63;
-  if (k > NG || k <= 0 || cap > 256) return false;
 #ifndef MR_NO_DPP
   if constexpr (GS <= 16) {
     group_best<GS>(mk, ms);
@@ -713,9 +714,26 @@ __device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long
   if (tid < 256) crank[tid] = 0;
   __syncthreads();
   stamp_at(sb, 10);
-  long long tk = gk[NG];
-  int tsg = gs[NG];
-  if (tk < 0) { tk = 0; tsg = INT_MAX; }  // fewer than k valid row bests: every valid key
+  tau_k = gk[NG];
+  tau_s = gs[NG];
+  if (tau_k < 0) { tau_k = 0; tau_s = INT_MAX; }  // fewer than k valid row bests: every valid key
+}
+
+// NG rows of NT / NG threads: more rows give a tighter tau (fewer survivors
+// to rank) for NG^2 / NT comparisons per thread.
+template <int NT, typename Get, int NG = NT / 16>
+__device__ __forceinline__ bool block_topk_threshold(int n, int k, Get get, long long mk, int ms, unsigned char* gm,
+                                                     long long* ck, int* cs, int cap, long long* out_k, int* out_s,
+                                                     long long* sb = nullptr, const TopkDst& dst = TopkDst{}) {
+  long long* gk = reinterpret_cast<long long*>(gm);
+  int* gs = reinterpret_cast<int*>(gk + NG + 1);
+  int* counter = gs + NG + 1;
+  int* crank = counter + 1 + NG;
+  const int tid = threadIdx.x;
+  if (k > NG || k <= 0 || cap > 256) return false;
+  long long tk;
+  int tsg;
+  block_tau<NT, NG>(k, mk, ms, gm, tk, tsg, sb);
   // (Compacting survivors per wave by ballot, one atomic per wave, measured
   // slower: C2 14.30 vs 14.11 us per step, profiles/r02/c2_topk_ab.txt.)
 #pragma unroll 4
@@ -1057,6 +1075,10 @@ struct ScoreParams {
   // score ([user] min, [mm_n + user] max; mr_dense_minmax), or null
   unsigned long long* mm_key;
   int mm_n;
+  // wide shape, top-k-only runs: the candidate-only tile top-k
+  // (wide_cand_topk) over fp32 approximations with 1/sqrt(c(s)) as fp32
+  int cand;
+  const float* rsq_c;
 };
 
 template <int MODEL, typename OutT, bool FUSED>
@@ -1733,6 +1755,88 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
   (void)v0;
 }
 
+// Candidate-only tile top-k of the wide kernel, for top-k-only runs (no
+// dense row, no min / max): the epilogue computes the exact fp64 score of
+// every song only to rank it, and ~k of a tile's ~19k songs leave the tile.
+// Here every song gets an fp32 approximation from its integer accumulator —
+// a ≈ acc / sqrt(c(s)) (ibm; acc for ubm) with a 4-B table of 1/sqrt(c) —
+// kept in registers (songs i = tid + NT e, e < EMAX); tau is the k-th best
+// row best of those (block_tau); only songs with a >= tau · (1 − 2^-17) get
+// the exact key (the same fp64 ops as the all-songs epilogue: the oracle's)
+// and are ranked exactly (rank_survivors).
+// Why no top-k song is lost: a carries ≤ 5·2^-24 relative error (the two
+// halves of acc converted, fma, the table's rounding, the product), the fp64
+// key ≤ 2^-52. The k songs behind tau have exact scores ≥ tau(1 − δ)/(1 + δ),
+// so the k-th best exact score is too, and any song ranked at or above it has
+// a ≥ tau(1 − 2δ − 2ε) > tau(1 − 2^-17). Ties of exact scores have equal
+// approximations (same acc, same c). Returns false, uniformly, when the
+// survivors overflow cap (e.g. fewer than k positive scores: tau = 0); acc
+// is untouched, so the caller then runs the all-songs path.
+template <int MODEL, int NT, int EMAX>
+__device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsigned long long* acc,
+                                               const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
+                                               long long* ck, int* cs, int cap, long long* fk, int* fs,
+                                               long long* sb) {
+  constexpr int NG = NT / 16;
+  const int tid = threadIdx.x;
+  float ap[EMAX];
+  long long mk = kKeyNone;
+  int ms = INT_MAX;
+  constexpr int EB = 10;  // songs per thread whose loads are issued together
+#pragma unroll
+  for (int e0 = 0; e0 < EMAX; e0 += EB) {
+    unsigned long long av[EB];
+    float rv[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int i = tid + (e0 + j) * NT;
+      av[j] = 0ull;
+      rv[j] = 0.f;
+      if (e0 + j < EMAX && i < bw) {
+        av[j] = acc[i];
+        rv[j] = MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int e = e0 + j;
+      if (e >= EMAX) continue;
+      const int i = tid + e * NT;
+      float a = -1.f;
+      if (i < bw && !((heard[i >> 5] >> (i & 31)) & 1u)) {
+        const float hi = (float)(unsigned)(av[j] >> 32), lo = (float)(unsigned)av[j];
+        a = __fmaf_rn(hi, 4294967296.f, lo) * rv[j];
+        take_if_before(mk, ms, (long long)__float_as_uint(a), blo + i);
+      }
+      ap[e] = a;
+    }
+  }
+  MR_STAMP(3);
+  long long tk;
+  int tsg;
+  block_tau<NT, NG>(k, mk, ms, gm, tk, tsg, sb);
+  int* counter = reinterpret_cast<int*>(reinterpret_cast<long long*>(gm) + NG + 1) + NG + 1;
+  int* crank = counter + 1 + NG;
+  const float thr = __uint_as_float((unsigned)tk) * (1.f - 0x1p-17f);  // tk = 0 (none): every song
+  const double inv_f = ldexp(1.0, -p.frac_bits);
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) {
+    if (ap[e] >= thr) {  // heard / past the tile: -1
+      const int i = tid + e * NT;
+      double score = (double)(long long)acc[i] * inv_f;
+      if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
+      const int pos = atomicAdd(counter, 1);
+      if (pos < cap) { ck[pos] = __double_as_longlong(score); cs[pos] = blo + i; }
+    }
+  }
+  __syncthreads();
+  const int nc = *counter;
+  if (nc > cap) return false;
+  rank_survivors<NT>(nc, k, ck, cs, crank, fk, fs);
+  return true;
+}
+constexpr int kCandE = 20;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
+
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
 template <int MODEL, typename OutT, int NT, int KS, bool COOC>
@@ -2010,6 +2114,17 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   __syncthreads();
   MR_STAMP(2);
 
+  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
+  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
+  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
+  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
+  const int k = KS == 10 ? 10 : p.topk;
+  // top-k-only runs: the candidate-only tile top-k (p.cand: no dense row, no
+  // min / max, 1 <= k <= NT / 16, bw <= kCandE * NT — set by the host)
+  bool have = false;
+  if (p.cand) have = wide_cand_topk<MODEL, NT, kCandE>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
+                                                        min(256, NW * k), fk, fs, nullptr);
+  if (!have) {
   // epilogue: scores -> dense row segment; keys back into acc. 8 songs per
   // thread per batch (the per-song scale loads in flight together), and the
   // thread's best key (thread_best order: i = tid + NT j) tracked on the way
@@ -2082,17 +2197,12 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       atomicMax(&p.mm_key[p.mm_n + u], ordered_key(b));
     }
   }
-  const int k = KS == 10 ? 10 : p.topk;
   if (p.topk <= 0) return;
   __syncthreads();
   MR_STAMP(3);
 
   // tile top-k: per-thread running lists (songs ascend per thread), per-wave
   // register tournament, then wave 0 over the NW wave lists.
-  long long* wk = reinterpret_cast<long long*>(smem_raw + L.wk);
-  int* ws = reinterpret_cast<int*>(smem_raw + L.ws);
-  long long* fk = reinterpret_cast<long long*>(smem_raw + L.fk);
-  int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   auto get_key = [&](int i, long long& key, int& song) { key = (long long)acc[i]; song = blo + i; };
   // (mk, ms): this thread's best key, from the epilogue
   const bool fast = !p.topk_lists && block_topk_threshold<NT>(bw, k, get_key, mk, ms, smem_raw + L.gm, wk, ws,
@@ -2113,6 +2223,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     if (w == 0) wave_merge_lists(NW, k, wk, ws, fk, fs);
     __syncthreads();
   }
+  }  // !have
   MR_STAMP(7);
   MR_STAMP(8);
   MR_STAMP(4);
@@ -3358,6 +3469,7 @@ enum Shape { kShapeSeparate = 0, kShapeFused = 1, kShapeWide = 3 };
 
 struct mr_ctx {
   mr_options opt{};
+  int dev_share = 1;  // contexts of this process on the device (mr_internal::set_device_share)
   hipStream_t stream = nullptr;
   bool loaded = false;
   bool ran = false;
@@ -3381,6 +3493,8 @@ struct mr_ctx {
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
+  DevBuf<float> rsq_c;  // wide shape: 1 / sqrt(c(s)) as fp32 (wide_cand_topk's approximations)
+  bool cand_on = false; // wide shape, top-k only: the candidate-only tile top-k (MR_WIDE_CAND=0: off)
   DevBuf<unsigned char> dense;
   DevBuf<long long> stamps;
   // Pinned staging of large D2H copies (d2h_staged): two buffers, lazily
@@ -3451,6 +3565,7 @@ struct mr_ctx {
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
+    rsq_c.release(); cand_on = false;
     dense.release();
     mm_key.release(); mm_on = mm_valid = false;
     stamps.release();
@@ -4031,10 +4146,12 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   const double two_f = std::ldexp(1.0, F);
   std::vector<double> sqrt_c(n_s), sqrt_tr(std::max(1, n_tr)), sqrt_te(n_te);
   std::vector<long long> q_song(n_s);
+  std::vector<float> rsq_c(n_s);
   mr_par::parallel_for(n_s, [&](int64_t a, int64_t b, int) {
     for (int64_t s2 = a; s2 < b; ++s2) {
       sqrt_c[s2] = std::sqrt((double)d->song_count[s2]);
       q_song[s2] = (long long)std::nearbyint(two_f / sqrt_c[s2]);
+      rsq_c[s2] = sqrt_c[s2] > 0.0 ? (float)(1.0 / sqrt_c[s2]) : 0.f;
     }
   });
   mr_par::parallel_for(n_tr, [&](int64_t a, int64_t b, int) {
@@ -4088,7 +4205,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   // MI355X; allocated at the first two-hop run, ensure_nbr)
   size_t free_b0 = 0, total_b0 = 0;
   MR_HIP(hipMemGetInfo(&free_b0, &total_b0));
-  const size_t budget = std::min<size_t>((size_t)32 << 30, std::max<size_t>((size_t)8 << 30, free_b0 / 8));
+  const size_t budget = std::min<size_t>((size_t)32 << 30, std::max<size_t>((size_t)8 << 30, free_b0 / 8)) /
+                        (size_t)std::max(1, c->dev_share);
   const int batch = fused ? n_te
                           : (int)std::max<size_t>(1, std::min<size_t>(std::min(n_te, 65528),
                                                                       budget / ((size_t)cap * 12)));
@@ -4129,6 +4247,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       te_row.resize(std::max<int64_t>(1, nte));
       for (int64_t i = 0; i < nte; ++i) te_row[i] = row_of[d->te_songs[i]];
       if (max_c > (int32_t)kCoocCntMask) why = "train listener counts < 131072";
+      // the row descriptors hold 32-bit listener-list starts and k_urec's
+      // records 32-bit shard-row bases (shard entries <= train entries)
+      else if (trs_off[n_s] >= (int64_t)INT32_MAX) why = "train entries < 2^31";
       else if ((long long)row_song.size() * n_tiles > INT32_MAX) why = "rows x tiles < 2^31";
     }
     if (!why && c->opt.ibm_route != 1) {
@@ -4282,6 +4403,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   if ((rc = dev_upload(c->trs_users, trs_users.data(), (size_t)trs_off[n_s], st))) return rc;
   if ((rc = dev_upload(c->q_song, q_song.data(), q_song.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_c, sqrt_c.data(), sqrt_c.size(), st))) return rc;
+  if (wide && (rc = dev_upload(c->rsq_c, rsq_c.data(), rsq_c.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_tr, sqrt_tr.data(), sqrt_tr.size(), st))) return rc;
   if ((rc = dev_upload(c->sqrt_te, sqrt_te.data(), sqrt_te.size(), st))) return rc;
   if ((rc = dev_upload(c->toff, toff.data(), toff.size(), st))) return rc;
@@ -4401,6 +4523,11 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->fused = fused;
   c->shape = shape;
   c->ibm_route = route;
+  {  // the candidate-only tile top-k (wide_cand_topk): top-k-only wide runs
+    const char* e = std::getenv("MR_WIDE_CAND");
+    c->cand_on = wide && !c->opt.dense && k >= 1 && k <= kWideThreads / 16 && !c->opt.topk_lists &&
+                 bs <= kCandE * kWideThreads && !(e && e[0] == '0');
+  }
   c->cooc_nt = cooc_nt_opt();
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
   pick_kernels<MR_UBM>(c);
@@ -4500,6 +4627,13 @@ int mr_route_info(const mr_ctx* c, int32_t* route, int32_t* n_rows, int64_t* poo
   if (route) *route = c->ibm_route;
   if (n_rows) *n_rows = c->n_rows;
   if (pool_entries) *pool_entries = c->pool_cap;
+  return MR_OK;
+}
+
+int mr_topk_mode(const mr_ctx* c, int32_t* candidate_only) {
+  if (!c || !candidate_only) return fail(MR_E_INVALID, "null argument");
+  if (!c->loaded) return fail(MR_E_STATE, "mr_topk_mode before mr_load");
+  *candidate_only = c->cand_on ? 1 : 0;
   return MR_OK;
 }
 
@@ -4748,6 +4882,7 @@ int run_cooc(mr_ctx* c) {
     sp.stamps = y0 == 0 ? c->stamps.p : nullptr;  // diagnostic build: the first launch
     sp.topk_lists = c->opt.topk_lists;
     if (c->mm_on) { sp.mm_key = c->mm_key.p; sp.mm_n = c->n_te; }
+    sp.cand = c->cand_on && !sp.mm_key; sp.rsq_c = c->rsq_c.p;
     hipLaunchKernelGGL(c->cooc_kernel, dim3(c->n_tiles, (ny + 7) / 8 * 8), dim3(c->cooc_nt), c->cooc_score_lds, st, sp);
     MR_HIP(hipGetLastError());
     if (k > 0 && c->n_tiles > 1) {
@@ -4850,6 +4985,7 @@ int run_model(mr_ctx* c, int model) {
       sp.stamps = c->stamps.p ? c->stamps.p + (size_t)y0 * c->n_tiles * kStampSlots : nullptr;
       sp.topk_lists = c->opt.topk_lists;
       if (c->mm_on && wide) { sp.mm_key = c->mm_key.p; sp.mm_n = c->n_te; }
+      sp.cand = wide && c->cand_on && !sp.mm_key; sp.rsq_c = c->rsq_c.p;
       hipLaunchKernelGGL(c->score_kernel[model], dim3(c->n_tiles, gy), dim3(wide ? kWideThreads : kThreads),
                          c->score_lds, st, sp);
       MR_HIP(hipGetLastError());
@@ -4997,6 +5133,12 @@ int topk_records(mr_ctx* c, void** records, int64_t* rec_bytes) {
 }
 
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+int set_device_share(mr_ctx* c, int n) {
+  if (!c || n < 1) return fail(MR_E_INVALID, "set_device_share: null context or share < 1");
+  c->dev_share = n;
+  return MR_OK;
+}
 
 int validate_dataset(const mr_dataset* d) {
   if (!d) return fail(MR_E_INVALID, "null dataset");

@@ -519,6 +519,11 @@ int mr_group_load(mr_group* g, const mr_dataset* d) {
         // the shard geometry is a creation option of a context: recreate it
         mr_ctx* c = nullptr;
         int r = mr_create(&oi, &c);
+        if (r == MR_OK) {  // contexts on the same device split its neighbour-list budget
+          int share = 0;
+          for (const Member& y : g->m) share += y.dev == x.dev ? 1 : 0;
+          r = mr_internal::set_device_share(c, share);
+        }
         if (r == MR_OK) r = mr_load(c, &views[x.block]);
         if (r != MR_OK) {
           msgs[i] = mr_last_error();

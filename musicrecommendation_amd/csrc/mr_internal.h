@@ -32,6 +32,12 @@ int validate_dataset(const mr_dataset* d);
 // context's pinned buffers when the destination is large pageable memory.
 int d2h_staged(mr_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch, size_t row_bytes, size_t rows);
 
+// Number of contexts of one process that share this context's device (set
+// by mr_group_load before mr_load, default 1): the lazily allocated neighbour
+// lists' budget (free device memory / 8 at load) is divided by it, since the
+// group's contexts measure free memory at once, before any of them allocates.
+int set_device_share(mr_ctx* c, int n);
+
 // Set the calling thread's mr_last_error() message; returns code.
 int set_error(int code, const char* msg);
 

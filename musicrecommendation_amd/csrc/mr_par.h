@@ -25,8 +25,8 @@ namespace mr_par {
 // CPU quota (on the GPU box hardware_concurrency() shows the whole machine
 // while the job gets a 16-core share), then shared with the other ranks of a
 // one-process-per-GPU launch on this node (torchrun's LOCAL_WORLD_SIZE: 8
-// ranks on a 16-core share get 2 threads each, not 16 each). MR_THREADS
-// overrides.
+// ranks on a 16-core share get 2 threads each, not 16 each) unless the
+// launcher already pinned each rank to its own CPU set. MR_THREADS overrides.
 inline int usable_cores() {
   static const int n = [] {
     if (const char* e = std::getenv("MR_THREADS")) {
@@ -43,12 +43,17 @@ inline int usable_cores() {
       char q[32] = {0};
       long long per = 0;
       if (std::fscanf(f, "%31s %lld", q, &per) == 2 && q[0] != 'm' && per > 0)
-        quota = (int)(std::atoll(q) / per);
+        quota = (int)std::max(1LL, std::atoll(q) / per);
       std::fclose(f);
     }
     int t = aff > 0 ? aff : 1;
+    // the ranks share the node's cores only when this rank's mask covers the
+    // whole share (the quota, else the machine); a launcher that pinned each
+    // rank to its own CPU set already split them
+    const int share = quota > 0 ? quota : (int)std::thread::hardware_concurrency();
+    const bool shared_mask = t >= share;
     if (quota > 0) t = std::min(t, quota);
-    t /= local_ranks;
+    if (shared_mask) t /= local_ranks;
     return std::max(1, std::min(t, 256));
   }();
   return n;

@@ -82,6 +82,10 @@ class Engine:
         # "two_hop" or "cooc" (co-listening index), and the index's size
         self.ibm_route = {1: "two_hop", 2: "cooc"}[rt.value]
         self.cooc_rows, self.cooc_pool_entries = nr.value, pe.value
+        co = ctypes.c_int32()
+        _lib.check(self._L.mr_topk_mode(self._h, ctypes.byref(co)), "mr_topk_mode")
+        # wide shape, top-k only: the tile top-k over fp32 approximations + exact candidates
+        self.candidate_topk = bool(co.value)
 
     # ---- lifecycle ----------------------------------------------------------
     def close(self) -> None:

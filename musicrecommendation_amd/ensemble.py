@@ -61,7 +61,8 @@ class DeviceEnsemble:
     context's dataset, i.e. a single-process run)."""
 
     def __init__(self, engine: Engine, *, pair_base: int = 0, n_pairs: Optional[int] = None,
-                 pos: Optional[np.ndarray] = None, n_label_songs: Optional[int] = None, group=None):
+                 pos: Optional[np.ndarray] = None, n_label_songs: Optional[int] = None, group=None,
+                 collectives: Optional[bool] = None):
         import torch
 
         from . import evaluation
@@ -76,6 +77,9 @@ class DeviceEnsemble:
         self.pos = evaluation.label_pos(self.ds) if pos is None else np.asarray(pos, dtype=np.int32)
         self.n_label_songs = int(self.ds.n_label_songs if n_label_songs is None else n_label_songs)
         self.group = group
+        # None: the MIN/MAX/SUM reductions run when the process group has more
+        # than one rank; True: always (a one-rank RCCL rehearsal of that path)
+        self.collectives = collectives
         self._host = None  # pinned (pred, tp) count buffers of threshold_map
 
     def empty(self):
@@ -145,9 +149,17 @@ class DeviceEnsemble:
         return outs
 
     def _minmax(self, t) -> Tuple[float, float]:
+        """Global min / max of a dense model (MR:524-525). The value carried by
+        the producing pass (model / combinations) is reused while torch's
+        version counter of `t` is unchanged: the cache assumes only torch
+        mutates the tensor — a write through its data_ptr from outside torch
+        (an engine call, DLPack) must be followed by t.add_(0) or a fresh
+        tensor, or the stale min / max is used. Otherwise the engine's min/max
+        kernel reads `t`, ordered after torch's pending work on it."""
         cached = getattr(t, "_mr_minmax", None)
         if cached is not None and cached[0] == t._version:  # from the producing pass, tensor unchanged
             return cached[1], cached[2]
+        self._after_torch()  # e.g. an in-place torch op on t still running on torch's stream
         return self.e.eval_minmax(t.data_ptr())
 
     # ---- evaluation --------------------------------------------------------------
@@ -155,6 +167,16 @@ class DeviceEnsemble:
         import torch.distributed as dist
 
         return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+
+    def _reduce(self) -> bool:
+        """Whether threshold_map all-reduces (more than one rank, or forced)."""
+        return self._world() > 1 or (bool(self.collectives) and self._pg())
+
+    @staticmethod
+    def _pg() -> bool:
+        import torch.distributed as dist
+
+        return dist.is_available() and dist.is_initialized()
 
     def threshold_map(self, t, n_thresholds: int = 10) -> float:
         """evaluateModel (MR:636) of a dense device model; n_thresholds = 11 is
@@ -165,7 +187,8 @@ class DeviceEnsemble:
         self._after_torch()
         mn, mx = self._minmax(t)
         world = self._world()
-        if world > 1:
+        reduce = self._reduce()
+        if reduce:
             be = dist.get_backend(self.group)
             dev = self.device if be == "nccl" else torch.device("cpu")
             a = torch.tensor([mn], dtype=torch.float64, device=dev)
@@ -175,7 +198,7 @@ class DeviceEnsemble:
             mn, mx = float(a.item()), float(b.item())
         if not (mn <= mx):
             raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
-        if world == 1 and self.e.song_lo == 0 and self.e.song_hi == self.ds.n_songs and hasattr(self.e, "eval_map"):
+        if not reduce and world == 1 and self.e.song_lo == 0 and self.e.song_hi == self.ds.n_songs and hasattr(self.e, "eval_map"):
             # one context holds the whole model: counts, AP per class on the device
             return self.e.eval_map(t.data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, self.pos,
                                    self.n_label_songs, n_thresholds=n_thresholds)
@@ -193,7 +216,7 @@ class DeviceEnsemble:
             full_t = np.zeros_like(full_p)
             full_p[self.e.song_lo:self.e.song_hi] = pred
             full_t[self.e.song_lo:self.e.song_hi] = tp
-        if world > 1:
+        if reduce:
             be = dist.get_backend(self.group)
             dev = self.device if be == "nccl" else torch.device("cpu")
             c = torch.from_numpy(np.stack([full_p, full_t])).to(dev)

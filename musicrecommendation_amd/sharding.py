@@ -215,6 +215,13 @@ class ShardScorer:
         self.out_keys = torch.empty((n_te, topk), dtype=torch.int64, device=self.device)
         self.out_scores = torch.empty((n_te, topk), dtype=torch.float64, device=self.device)
         self._ext = torch.cuda.ExternalStream(self.engine.stream, device=self.device)
+        # one song shard has nothing to exchange; True runs the all-gather +
+        # merge anyway (a one-rank rehearsal of the N > 1 collective path)
+        self.exchange_always = False
+
+    @property
+    def exchanges(self) -> bool:
+        return self.gs > 1 or self.exchange_always
 
     def pairs(self) -> int:
         """Scored pairs of this rank: its users x its songs, minus the heard ones."""
@@ -226,7 +233,7 @@ class ShardScorer:
         """Score the (block, shard) cell, then exchange + merge the block's top-k
         lists. Asynchronous: returns with the work queued on the streams."""
         self.engine.run(model)
-        if self.gs > 1:
+        if self.exchanges:
             self.exchange()
 
     def exchange(self) -> None:
@@ -260,7 +267,7 @@ class ShardScorer:
     def topk(self):
         """Merged (songs, keys) of this rank's user block, numpy (after step)."""
         self.sync()
-        if self.gs == 1:
+        if not self.exchanges:
             s, _sc, k = self.engine.topk()
             return s, k
         return self.out_songs.cpu().numpy(), self.out_keys.cpu().numpy()

@@ -106,8 +106,9 @@ def test_combinations_in_one_pass(dtype):
                     assert ens.threshold_map(got) == ens.threshold_map(exp)
                 carried = lin._mr_minmax[1:]
                 lin.mul_(2.0)  # in place: the carried min / max no longer apply
-                torch.cuda.synchronize()  # (the engine's stream does not wait on torch's here)
-                assert ens._minmax(lin) == e.eval_minmax(lin.data_ptr()) != carried
+                # no host sync: _minmax orders the engine's stream after torch's pending mul_
+                mm = ens._minmax(lin)
+                assert mm == e.eval_minmax(lin.data_ptr()) != carried
                 with pytest.raises(_lib.EngineError):
                     ens.combinations(u_t, i_t, 0.5, 1.5, 0.5)
 

@@ -162,3 +162,29 @@ def test_usable_cores_shared_by_local_ranks(monkeypatch):
     assert usable_cores() == max(1, full // 8)
     monkeypatch.setenv("MR_THREADS", "3")
     assert usable_cores() == 3
+
+
+def test_usable_cores_pinned_rank_keeps_its_mask(monkeypatch):
+    """A launcher that pinned each rank to its own CPU set (affinity mask
+    smaller than the node's share) already split the cores: no further
+    division by LOCAL_WORLD_SIZE."""
+    import os
+
+    from musicrecommendation_amd import mr_par_info
+
+    monkeypatch.delenv("MR_THREADS", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    monkeypatch.setattr(mr_par_info.os, "cpu_count", lambda: 64)
+    monkeypatch.setattr(mr_par_info.os, "sched_getaffinity", lambda pid: set(range(4)))
+    real_open = open
+
+    def no_cgroup(path, *a, **k):
+        if str(path) == "/sys/fs/cgroup/cpu.max":
+            raise OSError("no cgroup")
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", no_cgroup)
+    assert mr_par_info.usable_cores() == 4  # pinned to 4 of 64: kept
+    monkeypatch.setattr(mr_par_info.os, "sched_getaffinity", lambda pid: set(range(64)))
+    assert mr_par_info.usable_cores() == 16  # the whole machine: split 4 ways
+    assert os.cpu_count() is not None
