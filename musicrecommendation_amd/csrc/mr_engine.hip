@@ -1782,7 +1782,10 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
   float ap[EMAX];
   long long mk = kKeyNone;
   int ms = INT_MAX;
-  constexpr int EB = 10;  // songs per thread whose loads are issued together
+#ifndef MR_CAND_EB
+#define MR_CAND_EB 4
+#endif
+  constexpr int EB = MR_CAND_EB;  // songs per thread whose loads are issued together
 #pragma unroll
   for (int e0 = 0; e0 < EMAX; e0 += EB) {
     unsigned long long av[EB];
@@ -1812,22 +1815,32 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
     }
   }
   MR_STAMP(3);
+#if MR_CAND_STUB == 1
+  if (mk != -7) return false;
+#endif
   long long tk;
   int tsg;
   block_tau<NT, NG>(k, mk, ms, gm, tk, tsg, sb);
+#if MR_CAND_STUB == 2
+  if (tk != -7) return false;
+#endif
   int* counter = reinterpret_cast<int*>(reinterpret_cast<long long*>(gm) + NG + 1) + NG + 1;
   int* crank = counter + 1 + NG;
   const float thr = __uint_as_float((unsigned)tk) * (1.f - 0x1p-17f);  // tk = 0 (none): every song
   const double inv_f = ldexp(1.0, -p.frac_bits);
+  // the thread's survivors as a bit mask (heard / past the tile: a = -1), then
+  // a compact loop over the set bits (a few per tile: no unrolled 20-way body)
+  unsigned sm = 0u;
 #pragma unroll
-  for (int e = 0; e < EMAX; ++e) {
-    if (ap[e] >= thr) {  // heard / past the tile: -1
-      const int i = tid + e * NT;
-      double score = (double)(long long)acc[i] * inv_f;
-      if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
-      const int pos = atomicAdd(counter, 1);
-      if (pos < cap) { ck[pos] = __double_as_longlong(score); cs[pos] = blo + i; }
-    }
+  for (int e = 0; e < EMAX; ++e) sm |= ap[e] >= thr ? 1u << e : 0u;
+  while (sm) {
+    const int e = __builtin_ctz(sm);
+    sm &= sm - 1u;
+    const int i = tid + e * NT;
+    double score = (double)(long long)acc[i] * inv_f;
+    if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
+    const int pos = atomicAdd(counter, 1);
+    if (pos < cap) { ck[pos] = __double_as_longlong(score); cs[pos] = blo + i; }
   }
   __syncthreads();
   const int nc = *counter;
@@ -1835,7 +1848,10 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
   rank_survivors<NT>(nc, k, ck, cs, crank, fk, fs);
   return true;
 }
-constexpr int kCandE = 20;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
+#ifndef MR_CAND_E
+#define MR_CAND_E 20
+#endif
+constexpr int kCandE = MR_CAND_E;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
