@@ -204,7 +204,8 @@ int mr_cooc_stats(mr_ctx* ctx, int64_t* index_nnz, int64_t* consumed, int64_t* b
  *                   tile, or per tile group of k_cooc_group),
  *   consumed_bytes  Σ_u Σ_{s2 ∈ T(u)} Σ_t min(4 nnz(r, t), songs of t): the
  *                   segments the scoring kernel reads,
- *   group_tiles, n_groups  the heavy build's tile grouping.
+ *   group_tiles, n_groups  the heavy build's tile grouping,
+ *   index_* / consumed_*   the written encoding: sparse entries, dense songs.
  * MR_E_STATE unless the context is on route 2 and has run ibm since its load. */
 typedef struct mr_cooc_bytes_t {
   int64_t heavy_rows, light_rows;
@@ -214,6 +215,11 @@ typedef struct mr_cooc_bytes_t {
   int64_t consumed_bytes;
   int64_t group_tiles;  /* tiles per k_cooc_group pass (0: heavy rows per tile) */
   int64_t n_groups;     /* walks per u16 heavy row: tile groups, or n_tiles */
+  /* the encoding the build wrote: sparse entries (with the dense segments'
+   * excess entries) and the songs of dense segments, over the index and over
+   * the scoring's reads (each row's counts x the test users reading it) */
+  int64_t index_sparse_entries, index_dense_songs;
+  int64_t consumed_sparse_entries, consumed_dense_songs;
 } mr_cooc_bytes_t;
 int mr_cooc_bytes(mr_ctx* ctx, mr_cooc_bytes_t* out);
 

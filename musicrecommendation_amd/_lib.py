@@ -111,7 +111,8 @@ class MrCoocBytes(ctypes.Structure):
     """mr_cooc_bytes_t: encoding-independent byte counts of the co-listening route."""
     _fields_ = [(n, c_int64) for n in ("heavy_rows", "light_rows", "heavy_reads", "light_reads",
                                        "heavy_index_bytes", "light_index_bytes", "heavy_visits", "consumed_bytes",
-                                       "group_tiles", "n_groups")]
+                                       "group_tiles", "n_groups", "index_sparse_entries", "index_dense_songs",
+                                       "consumed_sparse_entries", "consumed_dense_songs")]
 
 
 MR_COMB_LINEAR = 0

@@ -4686,13 +4686,20 @@ int mr_cooc_bytes(mr_ctx* c, mr_cooc_bytes_t* out) {
   mr_cooc_bytes_t b{};
   for (int r = 0; r < nr; ++r) {
     int64_t seg = 0;  // Σ_t min(4 nnz(r, t), songs of t)
+    int64_t sp = 0, ds = 0;  // the written encoding: sparse entries, dense songs
     for (int t = 0; t < nt; ++t) {
       const int blo = c->song_lo + t * c->block_songs;
       const int64_t bw = std::min(c->song_hi, blo + c->block_songs) - blo;
       const int32_t l = len[(size_t)t * nr + r];
       // a dense segment (l <= kCoocDenseTail) holds >= bw / dense_div >= bw / 4 non-zeros
       seg += l >= 0 ? std::min<int64_t>(4 * (int64_t)l, bw) : bw;
+      if (l >= 0) sp += l;
+      else { ds += bw; sp += kCoocDenseTail - l; }
     }
+    b.index_sparse_entries += sp;
+    b.index_dense_songs += ds;
+    b.consumed_sparse_entries += sp * c->row_users[r];
+    b.consumed_dense_songs += ds * c->row_users[r];
     if (c->row_light[r]) {
       b.light_rows++;
       b.light_reads += c->row_reads[r];

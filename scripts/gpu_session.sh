@@ -197,5 +197,7 @@ case ",$STEPS," in *,profc4,*)
   export TMPDIR=/tmp
   run prof_c4 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4" -o bench -- python3 "$ROOT/bench.py" --config c4 --no-cpu-baseline --no-e2e --steps 3 --warmup 1 ;;
 esac
+# cost inputs of a song-factorised ubm route: the ibm index's encoding counts + both models' run times
+case ",$STEPS," in *,ubmcost,*) run ubm_cost 600 python -u scripts/ubm_cost.py ${UCFG:-c5} 3 ;; esac
 case ",$STEPS," in *,d2h,*) run d2h 300 python scripts/d2h_probe.py c3 3 ;; esac
 exit 0
