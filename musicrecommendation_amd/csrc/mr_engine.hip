@@ -1772,11 +1772,11 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
 // approximations (same acc, same c). Returns false, uniformly, when the
 // survivors overflow cap (e.g. fewer than k positive scores: tau = 0); acc
 // is untouched, so the caller then runs the all-songs path.
-template <int MODEL, int NT, int EMAX>
+template <int MODEL, int NT, int EMAX, bool PF>
 __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsigned long long* acc,
                                                const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
                                                long long* ck, int* cs, int cap, long long* fk, int* fs,
-                                               long long* sb) {
+                                               long long* sb, const float (&rq)[EMAX]) {
   constexpr int NG = NT / 16;
   const int tid = threadIdx.x;
   float ap[EMAX];
@@ -1797,7 +1797,8 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
       rv[j] = 0.f;
       if (e0 + j < EMAX && i < bw) {
         av[j] = acc[i];
-        rv[j] = MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f;
+        // PF: loaded at the kernel's start, in flight during stage 2
+        rv[j] = MODEL != MR_IBM ? 1.f : PF ? rq[e0 + j < EMAX ? e0 + j : 0] : p.rsq_c[blo + i];
       }
     }
 #pragma unroll
@@ -1843,6 +1844,7 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
     if (pos < cap) { ck[pos] = __double_as_longlong(score); cs[pos] = blo + i; }
   }
   __syncthreads();
+  stamp_at(sb, 11);
   const int nc = *counter;
   if (nc > cap) return false;
   rank_survivors<NT>(nc, k, ck, cs, crank, fk, fs);
@@ -1850,6 +1852,9 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
 }
 #ifndef MR_CAND_E
 #define MR_CAND_E 20
+#endif
+#ifndef MR_CAND_PF
+#define MR_CAND_PF 1  // wide_cand_topk's scales loaded at the scoring kernel's start (0: in pass A)
 #endif
 constexpr int kCandE = MR_CAND_E;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
 
@@ -1907,6 +1912,17 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     for (int e = 0; e < PF; ++e) {
       const int i = tid + e * NT;
       scp[e] = i < bw ? p.sqrt_c[blo + i] : 1.0;
+    }
+  }
+  // candidate-only top-k: this thread's 1/sqrt(c) scales (songs tid + NT e)
+  // loaded now, in flight while stage 2 runs (4 B each, 20 registers)
+  constexpr bool kCPF = MR_CAND_PF && MODEL == MR_IBM && COOC;
+  float rq[kCandE];
+  if constexpr (kCPF) {
+#pragma unroll
+    for (int e = 0; e < kCandE; ++e) {
+      const int i = tid + e * NT;
+      rq[e] = p.cand && i < bw ? p.rsq_c[blo + i] : 0.f;
     }
   }
   // co-listening route: the first descriptor pass's row lookups (te_row /
@@ -2138,8 +2154,16 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   // top-k-only runs: the candidate-only tile top-k (p.cand: no dense row, no
   // min / max, 1 <= k <= NT / 16, bw <= kCandE * NT — set by the host)
   bool have = false;
-  if (p.cand) have = wide_cand_topk<MODEL, NT, kCandE>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
-                                                        min(256, NW * k), fk, fs, nullptr);
+#ifdef MR_STAMPS
+  long long* sbp = p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr;
+#else
+  long long* sbp = nullptr;
+#endif
+  if (p.cand) {
+    have = wide_cand_topk<MODEL, NT, kCandE, kCPF>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
+                                                   min(256, NW * k), fk, fs, sbp, rq);
+    MR_STAMP(6);
+  }
   if (!have) {
   // epilogue: scores -> dense row segment; keys back into acc. 8 songs per
   // thread per batch (the per-song scale loads in flight together), and the

@@ -57,7 +57,7 @@ def test_candidate_lists_song_shards(c3_64, n_shards, monkeypatch):
         assert np.array_equal(s1, ts) and np.array_equal(k1, tk)
 
 
-@pytest.mark.parametrize("block", [256, 1000, 4096])
+@pytest.mark.parametrize("block", [256, 1024, 4096])
 def test_candidate_fixture_tiles(block, monkeypatch):
     """Small tiles (many per user), the fixtures' tiny users: tiles with fewer
     than k unheard or positive songs take the all-songs fallback."""
