@@ -1854,7 +1854,7 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
 #define MR_CAND_E 20
 #endif
 #ifndef MR_CAND_PF
-#define MR_CAND_PF 1  // wide_cand_topk's scales loaded at the scoring kernel's start (0: in pass A)
+#define MR_CAND_PF 0  // 1: wide_cand_topk's scales loaded at the scoring kernel's start (C4 41.5 vs 41.1 ms)
 #endif
 constexpr int kCandE = MR_CAND_E;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
 
@@ -4563,12 +4563,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   c->fused = fused;
   c->shape = shape;
   c->ibm_route = route;
+  c->cooc_nt = cooc_nt_opt();
   {  // the candidate-only tile top-k (wide_cand_topk): top-k-only wide runs
     const char* e = std::getenv("MR_WIDE_CAND");
-    c->cand_on = wide && !c->opt.dense && k >= 1 && k <= kWideThreads / 16 && !c->opt.topk_lists &&
-                 bs <= kCandE * kWideThreads && !(e && e[0] == '0');
+    const int nt = route == 2 ? c->cooc_nt : kWideThreads;  // the scoring kernel's threads
+    c->cand_on = wide && !c->opt.dense && k >= 1 && k <= nt / 16 && !c->opt.topk_lists && bs <= kCandE * nt &&
+                 !(e && e[0] == '0');
   }
-  c->cooc_nt = cooc_nt_opt();
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;
   pick_kernels<MR_UBM>(c);
   pick_kernels<MR_IBM>(c);
