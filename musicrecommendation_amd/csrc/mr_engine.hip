@@ -2328,6 +2328,12 @@ struct CoocParams {
   // tile's entries, tiles 0..n_tiles — and the tile groups (grp tiles each)
   const unsigned* urec;
   int urec_words, grp, n_grp;
+  // k_cooc_group: per (row, listener) a record of lrec_words u32 words — word
+  // 0 the listener's first entry in sr_songs, then u16 starts (relative to
+  // it) of every tile group g = 0..n_grp — in the row's listener order, the
+  // row's first record at rdesc.z (built at load by k_lrec from urec)
+  const unsigned* lrec;
+  int lrec_words;
   long long* lstamps;            // diagnostic build: [light row of the launch][8] (k_cooc_light*)
   // k_cooc_light* / k_cooc_group: the launch's rows as {row, row_slots value,
   // first listener in trs_users, listeners} (one load instead of rows ->
@@ -2626,8 +2632,8 @@ __device__ __forceinline__ void light_insert(unsigned* tab, unsigned mask, int s
 #ifndef MR_WALK_R
 #define MR_WALK_R 2  // listeners per lane group per iteration of rows_walk (loads issued together)
 #endif
-template <typename Range, typename Ins>
-__device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, const int* lst, int n, Range&& range,
+template <typename Ids, typename Range, typename Ins>
+__device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, Ids&& lst, int n, Range&& range,
                                           const unsigned* sr_songs, Ins&& ins) {
   constexpr int R = MR_WALK_R;
   const int G = 1 << glog;
@@ -2657,8 +2663,8 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
   for (int r = 0; r < R; ++r) {
     const int l = grp + r * step, l1 = l + stride;
     a0[r] = b0[r] = 0;
-    if (l < n) range(lst[l], a0[r], b0[r]);
-    v1[r] = l1 < n ? lst[l1] : -1;
+    if (l < n) range(lst(l), a0[r], b0[r]);
+    v1[r] = l1 < n ? lst(l1) : -1;
   }
   for (int l0 = grp; l0 < n; l0 += stride) {
     u32x4_a4 c[R][2];
@@ -2676,7 +2682,7 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, co
       a1[r] = b1[r] = 0;
       if (v1[r] >= 0) range(v1[r], a1[r], b1[r]);
       const int l2 = l0 + 2 * stride + r * step;
-      v2[r] = l2 < n ? lst[l2] : -1;
+      v2[r] = l2 < n ? lst(l2) : -1;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) put2(c[r][0], m[r][0], c[r][1], m[r][1]);
@@ -2778,7 +2784,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   const int* lst = p.trs_users + (unsigned)rd.z;
   __syncthreads();  // the table and the tile counters are zero
   stamp_rt(sb, 1);
-  rows_walk(tid, NT, rd.y >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+  rows_walk(tid, NT, rd.y >> kLightGlogShift, [&](int l) { return lst[l]; }, n, shard_row(p), p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   __syncthreads();
   stamp_rt(sb, 2);
@@ -2856,7 +2862,7 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   const int* lst = p.trs_users + (unsigned)rd.z;
   wave_lds_sync();  // the table and the tile counters are zero
   stamp_rt_wave(sb, 1);
-  rows_walk(lane, 64, rd.y >> kLightGlogShift, lst, n, shard_row(p), p.sr_songs,
+  rows_walk(lane, 64, rd.y >> kLightGlogShift, [&](int l) { return lst[l]; }, n, shard_row(p), p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
@@ -3039,16 +3045,17 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
   *off = o;
 }
 
-// range of rows_walk: listener v's entries of tiles [t0, t1)
+// range of rows_walk: record x's entries of tile group g (lrec: the
+// listener's base and group starts, one 16-B record in the row's order)
 struct GroupRange {
   const unsigned* rec;
-  int words, t0, t1;
-  __device__ __forceinline__ void operator()(int v, long long& a, long long& b) const {
-    const unsigned* q = rec + (size_t)v * words;
+  int words, g;
+  __device__ __forceinline__ void operator()(int x, long long& a, long long& b) const {
+    const unsigned* q = rec + (size_t)x * words;
     const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
     const long long base = q[0];
-    a = base + st[t0];
-    b = base + st[t1];
+    a = base + st[g];
+    b = base + st[g + 1];
   }
 };
 
@@ -3101,32 +3108,33 @@ __device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int 
 #endif
 constexpr int kGroupPipeR = MR_GROUP_PIPE_R;
 template <int NT>
-__device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const int* lst, int n, int glog,
+__device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const unsigned* lst, int n, int glog,
                                                      int width, unsigned* cnt, int* s_wcnt, int* s_tail,
                                                      long long* sb, long long* off, unsigned* row_nz) {
   constexpr int R = kGroupPipeR;
   const int tid = threadIdx.x;
   const int L = 1 << glog, j = tid & (L - 1), lg = tid >> glog, step = NT >> glog;
-  const int bs = p.block_songs, GT = p.grp, nt = p.n_tiles, ng = p.n_grp, words = p.urec_words;
+  const int bs = p.block_songs, GT = p.grp, nt = p.n_tiles, ng = p.n_grp, words = p.lrec_words;
   const unsigned* songs = p.sr_songs;
-  // listener i of this lane group: lg + i * step; its entries of the current
-  // group: [a, b) of sr_songs (records hold 32-bit bases, mr_load)
+  // listener i of this lane group: record lg + i * step of the row (lst: the
+  // row's first record); its entries of the current group: [a, b) of
+  // sr_songs (records hold 32-bit bases, mr_load)
   int v[R];
   unsigned base[R], a[R], b[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int l = lg + i * step;
-    v[i] = l < n ? lst[l] : -1;
+    v[i] = l < n ? l : -1;
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     base[i] = a[i] = b[i] = 0u;
     if (v[i] >= 0) {
-      const unsigned* q = p.urec + (size_t)v[i] * words;
+      const unsigned* q = lst + (size_t)v[i] * words;
       const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
       base[i] = q[0];
       a[i] = base[i] + st[0];
-      b[i] = base[i] + st[min(nt, GT)];
+      b[i] = base[i] + st[1];
     }
   }
   u32x4_a4 c[R][2];
@@ -3138,7 +3146,7 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
     m[i][1] = group_chunk(songs, x + 4u * L, b[i], c[i][1]);
   }
   for (int gi = 0; gi < ng; ++gi) {
-    const int t0 = gi * GT, t1 = min(nt, t0 + GT), t2 = min(nt, t1 + GT);
+    const int t0 = gi * GT, t1 = min(nt, t0 + GT);
     const unsigned lo0 = (unsigned)(t0 * bs);  // shard-local first song of the group
     const int gw = min(width, t1 * bs) - t0 * bs;
     group_zero<NT>(cnt, gw, s_tail);
@@ -3148,7 +3156,7 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
     for (int i = 0; i < R; ++i) {
       e[i] = b[i];
       if (v[i] >= 0 && gi + 1 < ng)
-        e[i] = base[i] + reinterpret_cast<const unsigned short*>(p.urec + (size_t)v[i] * words + 1)[t2];
+        e[i] = base[i] + reinterpret_cast<const unsigned short*>(lst + (size_t)v[i] * words + 1)[gi + 2];
     }
     __syncthreads();
 #pragma unroll
@@ -3218,7 +3226,9 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   const int4 rd = p.rdesc[ri];
   const int r = rd.x;
   const int n = rd.w;
-  const int* lst = p.trs_users + (unsigned)rd.z;
+  // the row's listener records (lrec, from rd.z): no listener id, no per-user
+  // record line on the way to the shard-row chunks
+  const unsigned* lst = p.lrec + (size_t)(unsigned)rd.z * p.lrec_words;
   const int glog = rd.y >> kLightGlogShift;
   long long* sb = p.stamps ? p.stamps + (size_t)blockIdx.x * 8 : nullptr;
   stamp_rt(sb, 0);
@@ -3237,7 +3247,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     group_zero<NT>(cnt, gw, s_tail);
     __syncthreads();
     // fire-and-forget adds (no returned value, no per-entry bookkeeping)
-    rows_walk(tid, NT, glog, lst, n, GroupRange{p.urec, p.urec_words, t0, t1}, p.sr_songs,
+    rows_walk(tid, NT, glog, [](int l) { return l; }, n, GroupRange{lst, p.lrec_words, gi}, p.sr_songs,
               [&](const unsigned (&k)[8], int m) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
@@ -3277,6 +3287,24 @@ __global__ __launch_bounds__(256) void k_urec(const long long* sr_off, const uns
     const unsigned lim = (unsigned)t * (unsigned)bs;
     while (x < b && sr_songs[x] < lim) ++x;
     st[t] = (unsigned short)(t == n_tiles ? b - a : x - a);
+  }
+}
+
+// k_cooc_group's per-(row, listener) records, built once per load from the
+// per-user records: one workgroup per u16 heavy row (rd.z: its first record,
+// rd.w: its listeners), the listener's base and its tile-group starts.
+__global__ __launch_bounds__(256) void k_lrec(const int4* rdesc, const int* row_song, const long long* trs_off,
+                                              const int* trs_users, const unsigned* urec, int urec_words,
+                                              int n_tiles, int grp, int n_grp, int words, unsigned* lrec) {
+  const int4 rd = rdesc[blockIdx.x];
+  const long long s0 = trs_off[row_song[rd.x]];
+  for (int l = threadIdx.x; l < rd.w; l += 256) {
+    const unsigned* q = urec + (size_t)trs_users[s0 + l] * urec_words;
+    const unsigned short* st = reinterpret_cast<const unsigned short*>(q + 1);
+    unsigned* o = lrec + (size_t)((unsigned)rd.z + l) * words;
+    o[0] = q[0];
+    unsigned short* os = reinterpret_cast<unsigned short*>(o + 1);
+    for (int g = 0; g < 2 * (words - 1); ++g) os[g] = g <= n_grp ? st[min(n_tiles, g * grp)] : 0;
   }
 }
 
@@ -3594,8 +3622,9 @@ struct mr_ctx {
   DevBuf<int4> rdesc;              // rows_order's rows as {row, row_slots, listener start, listeners}
   DevBuf<long long> sr_off;        // light rows / k_cooc_group: the shard's train rows
   DevBuf<unsigned> sr_songs;
-  DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts
-  int grp = 0, n_grp = 0, urec_words = 0;
+  DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts (load-time only: lrec's source)
+  DevBuf<unsigned> lrec;           // k_cooc_group: per-(row, listener) base + tile-group starts
+  int grp = 0, n_grp = 0, urec_words = 0, lrec_words = 0;
   int group_nt = 1024;             // threads per k_cooc_group workgroup (MR_COOC_GNT)
 
   void release_data() {
@@ -3613,7 +3642,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    urec.release(); rdesc.release(); grp = n_grp = urec_words = 0;
+    urec.release(); lrec.release(); rdesc.release(); grp = n_grp = urec_words = lrec_words = 0;
     row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -4262,7 +4291,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   int dense_div = kCoocDenseDiv;
   int n_heavy32 = 0, n_big16 = 0, tcap16 = 0, tcap32 = 0;
   int32_t max_shard_deg = 0;
-  int grp = 0, n_grp = 0, urec_words = 0;  // k_cooc_group (0: the per-tile k_cooc_build)
+  int grp = 0, n_grp = 0, urec_words = 0, lrec_words = 0;  // k_cooc_group (0: the per-tile k_cooc_build)
   std::vector<int64_t> row_reads;
   int64_t pool_cap = 0;
   {
@@ -4496,11 +4525,18 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
+    int64_t n_lrec = 0;  // k_cooc_group's records: the u16 heavy rows' listeners
     {
       std::vector<int4> rd(std::max<size_t>(1, order.size()));
       for (size_t i = 0; i < order.size(); ++i) {
         const int32_t r = order[i], s2 = row_song[r];
-        rd[i] = make_int4(r, row_slots[r], (int)trs_off[s2], (int)(trs_off[s2 + 1] - trs_off[s2]));
+        const int cnt = (int)(trs_off[s2 + 1] - trs_off[s2]);
+        int z = (int)trs_off[s2];  // the first listener in trs_users
+        if (grp > 0 && (int)i >= n_heavy32 && i < heavy_rows.size()) {  // the first record in lrec
+          z = (int)n_lrec;
+          n_lrec += cnt;
+        }
+        rd[i] = make_int4(r, row_slots[r], z, cnt);
       }
       if ((rc = dev_upload(c->rdesc, rd.data(), rd.size(), st))) return rc;
       MR_HIP(hipStreamSynchronize(st));
@@ -4529,11 +4565,22 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       });
       if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
       if ((rc = dev_upload(c->sr_songs, ss.data(), ss.size(), st))) return rc;
-      if (grp > 0) {  // k_cooc_group's per-user records (tile starts), on the device
+      if (grp > 0) {  // k_cooc_group's records, on the device: per user (tile starts), then per (row, listener)
         if ((rc = dev_alloc(c->urec, (size_t)std::max(1, n_tr) * urec_words))) return rc;
         hipLaunchKernelGGL(k_urec, dim3((std::max(1, n_tr) + 255) / 256), dim3(256), 0, st, c->sr_off.p,
                            c->sr_songs.p, n_tr, n_tiles, bs, urec_words, c->urec.p);
         MR_HIP(hipGetLastError());
+        lrec_words = 1;  // base + (n_grp + 1) u16 starts, a power of 2 of words
+        while (2 * (lrec_words - 1) < n_grp + 1) lrec_words <<= 1;
+        if ((rc = dev_alloc(c->lrec, (size_t)std::max<int64_t>(1, n_lrec) * lrec_words))) return rc;
+        const int n16 = (int)heavy_rows.size() - n_heavy32;
+        if (n16 > 0)
+          hipLaunchKernelGGL(k_lrec, dim3(n16), dim3(256), 0, st, c->rdesc.p + n_heavy32, c->row_song.p,
+                             c->trs_off.p, c->trs_users.p, c->urec.p, urec_words, n_tiles, grp, n_grp, lrec_words,
+                             c->lrec.p);
+        MR_HIP(hipGetLastError());
+        MR_HIP(hipStreamSynchronize(st));
+        c->urec.release();  // (lrec holds what the runs need)
       }
       MR_HIP(hipStreamSynchronize(st));  // so / ss die here
     }
@@ -4611,6 +4658,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->grp = grp;
     c->n_grp = n_grp;
     c->urec_words = urec_words;
+    c->lrec_words = lrec_words;
     c->group_nt = cooc_group_nt_opt();
     if (grp > 0)
       MR_HIP(hipFuncSetAttribute(c->group_nt == 512 ? (const void*)k_cooc_group<512> : (const void*)k_cooc_group<1024>,
@@ -4863,8 +4911,8 @@ int run_cooc(mr_ctx* c) {
       hp.rows = c->rows_order.p + n32;
       hp.n_big = c->n_big16;
       hp.tcap = c->tcap16;
-      hp.urec = c->urec.p;
-      hp.urec_words = c->urec_words;
+      hp.lrec = c->lrec.p;
+      hp.lrec_words = c->lrec_words;
       hp.grp = c->grp;
       hp.n_grp = c->n_grp;
       hp.rdesc = c->rdesc.p + n32;

@@ -199,5 +199,13 @@ case ",$STEPS," in *,profc4,*)
 esac
 # cost inputs of a song-factorised ubm route: the ibm index's encoding counts + both models' run times
 case ",$STEPS," in *,ubmcost,*) run ubm_cost 600 python -u scripts/ubm_cost.py ${UCFG:-c5} 3 ;; esac
+# PMC passes of one C4 step (scripts/pmc_bulk.sh) per library variant: PMCVARS="prod urec"
+case ",$STEPS," in *,pmcvar,*)
+  for v in ${PMCVARS:-prod}; do
+    lib=$v; [ "$v" = prod ] && lib=""
+    tag=""; [ "$v" != prod ] && tag="_$v"
+    MR_ENGINE_LIB=$lib TAG=$tag run pmcvar_$v 1500 bash scripts/pmc_bulk.sh
+  done ;;
+esac
 case ",$STEPS," in *,d2h,*) run d2h 300 python scripts/d2h_probe.py c3 3 ;; esac
 exit 0
