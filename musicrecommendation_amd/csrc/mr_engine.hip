@@ -2950,7 +2950,7 @@ __device__ __forceinline__ int nz_pairs8(const uint4& w) {
 template <int NT>
 __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bool big, int t0, int ntg, int bs,
                                                   int width, const unsigned* cnt, int* s_wcnt, int* s_tail,
-                                                  long long* off, unsigned* row_nz) {
+                                                  long long* off, unsigned* row_nz, long long* sb = nullptr) {
   constexpr int NW = NT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int k = 0; k < ntg; ++k) {
@@ -2963,6 +2963,7 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     if (lane == 0) s_wcnt[k * NW + w] = ws;
   }
   __syncthreads();
+  stamp_rt(sb, 3);  // (diagnostic build: pass A of the first group)
   // tile k's non-zeros, and this wave's first entry among them (lane x reads
   // wave x's count; one scan, two lane reads)
   const int ws_id = __builtin_amdgcn_readfirstlane(w);
@@ -3186,7 +3187,8 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
         m[i][1] = group_chunk(songs, x + 4u * L, b[i], c[i][1]);
       }
     }
-    cooc_emit_group16<NT>(p, r, false, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, off, row_nz);
+    cooc_emit_group16<NT>(p, r, false, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, off, row_nz,
+                          gi == 0 ? sb : nullptr);
     // thread 0 reads s_wcnt / s_tail after the emission's closing barrier: keep
     // the next group's zeroing behind it
     __syncthreads();
@@ -3259,7 +3261,8 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
     // tile k's counters start at word k * bs / 2 (bs is a multiple of 256: 16-B aligned)
-    cooc_emit_group16<NT>(p, r, big, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, &off, &row_nz);
+    cooc_emit_group16<NT>(p, r, big, t0, t1 - t0, bs, width, cnt, s_wcnt, s_tail, &off, &row_nz,
+                          gi == g_begin ? sb : nullptr);
     // thread 0 reads s_wcnt / s_tail after the emission's closing barrier: keep
     // the next group's zeroing behind it (the dc4df36 race class)
     __syncthreads();

@@ -60,9 +60,16 @@ if len(B):
     dur = (B[:, 4] - B[:, 0]) * tick_us
     print(f" heavy WGs {len(B)} (big {int(B[:, 5].sum())}), span {(B[:, 4].max() - B[:, 0].min()) * tick_us / 1e3:.2f} ms, "
           f"sum(WG time)/256 {dur.sum() / 256 / 1e3:.2f} ms")
-    for name, a, b in (("first walk", 0, 1), ("first emit", 1, 2), ("rest", 2, 4)):
-        v = (B[:, b] - B[:, a]) * tick_us
-        print(f"    {name:10s} med {np.median(v):8.1f} us p90 {np.percentile(v, 90):8.1f} share {v.sum() / dur.sum():.3f}")
+    g = B[:, 3] >= B[:, 1]  # group-kernel workgroups (stamp 3: the first group's emission pass A)
+    for kind, sel in (("pipelined rows", g & (B[:, 5] == 0)), ("big rows (row, group)", g & (B[:, 5] == 1))):
+        if not sel.any():
+            continue
+        print(f"   {kind}: WGs {sel.sum()} med {np.median(dur[sel]):8.1f} us, share {dur[sel].sum() / dur.sum():.3f}")
+        for name, a, b in (("first walk", 0, 1), ("first emit", 1, 2), (" pass A", 1, 3), (" pass B", 3, 2),
+                           ("rest", 2, 4)):
+            v = (B[sel, b] - B[sel, a]) * tick_us
+            print(f"    {name:10s} med {np.median(v):8.1f} us p90 {np.percentile(v, 90):8.1f} "
+                  f"share {v.sum() / dur[sel].sum():.3f}")
     n = B[:, 6]
     for lo_, hi_ in ((0, 4096), (4096, 16384), (16384, 1 << 30)):
         m = (n >= lo_) & (n < hi_)

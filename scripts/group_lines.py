@@ -88,7 +88,8 @@ def main():
            "big_rows": int(big.sum()), "pipelined_rows": int((~big).sum())}
     # per (row, listener) over the u16 heavy rows
     parts = {k: 0 for k in ("ids_bytes", "rows_bytes", "ids_lines_lower", "ids_lines_upper", "urec_lines_lower",
-                            "urec_lines_upper", "sr_lines_lower", "sr_lines_upper", "sr_lines_per_group_walk")}
+                            "urec_lines_upper", "sr_lines_lower", "sr_lines_upper", "sr_lines_per_group_walk",
+                            "sr_lines_upper_aligned", "lrec_lines_upper")}
     hist = {}
     for is_big in (True, False):
         rows = h16[big] if is_big else h16[~big]
@@ -114,13 +115,18 @@ def main():
             nz = hi_all > lo_all
             parts["sr_lines_lower"] += int(span_lines(lo_all[nz], hi_all[nz] + 3).sum())
             tot = np.zeros(lst.size, np.int64)
+            tal = np.zeros(lst.size, np.int64)
             for g in range(NG):
                 aa = base + st[lst, g * GRP]
                 bb = base + st[lst, min(NT, (g + 1) * GRP)]
                 m = bb > aa
                 last = aa + 4 * ((bb - 1 - aa) // 4) + 3  # the last 16-B chunk's last entry
                 tot[m] += span_lines(aa[m], last[m] + 1)
+                tal[m] += span_lines(aa[m], bb[m])  # 16-B-aligned chunks: the lines of [a, b) only
             parts["sr_lines_upper"] += int(tot.sum())
+            parts["sr_lines_upper_aligned"] += int(tal.sum())
+            # per-(row, listener) 16-B records (lrec), contiguous: per row, per group for big rows
+            parts["lrec_lines_upper"] += int(np.ceil(16 * lst.size / LINE) * (NG if is_big else 1))
             parts["sr_lines_per_group_walk"] += int(tot.sum())
         ct = c_tr[rows]
         for lo_, hi_ in ((0, 256), (256, 1024), (1024, 2048), (2048, 8192), (8192, 65536)):
@@ -136,6 +142,8 @@ def main():
         "urec_records": [parts["urec_lines_lower"] * LINE / GB, parts["urec_lines_upper"] * LINE / GB],
         "shard_row_chunks": [parts["sr_lines_lower"] * LINE / GB, parts["sr_lines_upper"] * LINE / GB],
     }
+    res["shard_row_chunks_aligned_upper_GB"] = parts["sr_lines_upper_aligned"] * LINE / GB
+    res["lrec_records_upper_GB"] = parts["lrec_lines_upper"] * LINE / GB
     lo = sum(v[0] for v in res["line_model_GB"].values())
     hi = sum(v[1] for v in res["line_model_GB"].values())
     res["line_model_total_GB"] = [lo, hi]
