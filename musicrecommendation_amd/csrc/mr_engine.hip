@@ -2686,25 +2686,14 @@ __device__ __forceinline__ void rows_walk(int lane_id, int n_lanes, int glog, Id
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) put2(c[r][0], m[r][0], c[r][1], m[r][1]);
-    // longer rows: the R listeners' next chunks issued together each step
-    long long xs[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) xs[r] = a0[r] + 4 * j + 8 * G;
-    for (;;) {
-      bool more = false;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        more |= xs[r] < b0[r];
-        m[r][0] = chunk(xs[r], b0[r], c[r][0]);
-        m[r][1] = chunk(xs[r] + 4 * G, b0[r], c[r][1]);
+    for (int r = 0; r < R; ++r)
+      for (long long x = a0[r] + 4 * j + 8 * G; x < b0[r]; x += 8 * G) {
+        u32x4_a4 c0, c1;
+        const int m0 = chunk(x, b0[r], c0);
+        const int m1 = chunk(x + 4 * G, b0[r], c1);
+        put2(c0, m0, c1, m1);
       }
-      if (!more) break;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        put2(c[r][0], m[r][0], c[r][1], m[r][1]);
-        xs[r] += 8 * G;
-      }
-    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       a0[r] = a1[r];
@@ -3119,7 +3108,6 @@ __device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int 
 #define MR_GROUP_PIPE_R 4
 #endif
 constexpr int kGroupPipeR = MR_GROUP_PIPE_R;
-static_assert(kGroupPipeR % 2 == 0, "cooc_group_pipelined walks its listeners' tails in pairs");
 template <int NT>
 __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r, const unsigned* lst, int n, int glog,
                                                      int width, unsigned* cnt, int* s_wcnt, int* s_tail,
@@ -3177,26 +3165,15 @@ __device__ __forceinline__ void cooc_group_pipelined(const CoocParams& p, int r,
       group_add(cnt, c[i][0], m[i][0], lo0);
       group_add(cnt, c[i][1], m[i][1], lo0);
     }
-    // the parts past the prefetched chunks: two listeners' next two chunks
-    // issued together, then added (one memory round trip per step for the
-    // pair, not one per listener and step)
 #pragma unroll
-    for (int i0 = 0; i0 < R; i0 += 2) {
-      unsigned x0 = a[i0] + 4u * j + 8u * L, x1 = a[i0 + 1] + 4u * j + 8u * L;
-      while (x0 < b[i0] || x1 < b[i0 + 1]) {
-        u32x4_a4 d0, d1, d2, d3;
-        const int m0 = group_chunk(songs, x0, b[i0], d0);
-        const int m1 = group_chunk(songs, x0 + 4u * L, b[i0], d1);
-        const int m2 = group_chunk(songs, x1, b[i0 + 1], d2);
-        const int m3 = group_chunk(songs, x1 + 4u * L, b[i0 + 1], d3);
+    for (int i = 0; i < R; ++i)
+      for (unsigned x = a[i] + 4u * j + 8u * L; x < b[i]; x += 8u * L) {
+        u32x4_a4 d0, d1;
+        const int m0 = group_chunk(songs, x, b[i], d0);
+        const int m1 = group_chunk(songs, x + 4u * L, b[i], d1);
         group_add(cnt, d0, m0, lo0);
         group_add(cnt, d1, m1, lo0);
-        group_add(cnt, d2, m2, lo0);
-        group_add(cnt, d3, m3, lo0);
-        x0 += 8u * L;
-        x1 += 8u * L;
       }
-    }
     __syncthreads();
     if (gi == 0) stamp_rt(sb, 1);  // the first group's walk done
     // the next group's first chunks: in flight while this group is emitted
