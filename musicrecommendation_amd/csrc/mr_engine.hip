@@ -1760,12 +1760,10 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
 // every song only to rank it, and ~k of a tile's ~19k songs leave the tile.
 // Here every song gets an fp32 approximation from its integer accumulator —
 // a ≈ acc / sqrt(c(s)) (ibm; acc for ubm) with a 4-B table of 1/sqrt(c) —
-// kept in registers (cand_pass_a over songs i = tid + NT e, or on the
-// co-listening route the last dense pass itself, which forms every song's
-// final accumulator); tau is the k-th best row best of those (block_tau);
-// only songs with a >= tau · (1 − 2^-17) get the exact key (the same fp64 ops
-// as the all-songs epilogue: the oracle's) and are ranked exactly
-// (cand_select, rank_survivors). Together: "wide_cand_topk".
+// kept in registers (songs i = tid + NT e, e < EMAX); tau is the k-th best
+// row best of those (block_tau); only songs with a >= tau · (1 − 2^-17) get
+// the exact key (the same fp64 ops as the all-songs epilogue: the oracle's)
+// and are ranked exactly (rank_survivors).
 // Why no top-k song is lost: a carries ≤ 5·2^-24 relative error (the two
 // halves of acc converted, fma, the table's rounding, the product), the fp64
 // key ≤ 2^-52. The k songs behind tau have exact scores ≥ tau(1 − δ)/(1 + δ),
@@ -1774,107 +1772,76 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
 // approximations (same acc, same c). Returns false, uniformly, when the
 // survivors overflow cap (e.g. fewer than k positive scores: tau = 0); acc
 // is untouched, so the caller then runs the all-songs path.
-// One song's fp32 approximation: acc (two u32 halves converted, fma) x its
-// 1/sqrt(c) (ibm; 1 for ubm).
-__device__ __forceinline__ float cand_approx(unsigned long long v, float r) {
-  const float hi = (float)(unsigned)(v >> 32), lo = (float)(unsigned)v;
-  return __fmaf_rn(hi, 4294967296.f, lo) * r;
-}
-
-// A thread's three best approximations, (a desc, song asc); a = -1: none.
-// Survivors beyond the third are found by a rescan of the thread's songs
-// (cand_select), so three registers pairs replace one per song.
-struct CandTop3 {
-  float a[3] = {-1.f, -1.f, -1.f};
-  int s[3] = {INT_MAX, INT_MAX, INT_MAX};
-  __device__ __forceinline__ static bool before(float a0, int s0, float a1, int s1) {
-    return a0 > a1 || (a0 == a1 && s0 < s1);
-  }
-  __device__ __forceinline__ void insert(float x, int song) {
-    if (!before(x, song, a[2], s[2])) return;
-    if (before(x, song, a[1], s[1])) {
-      a[2] = a[1]; s[2] = s[1];
-      if (before(x, song, a[0], s[0])) { a[1] = a[0]; s[1] = s[0]; a[0] = x; s[0] = song; }
-      else { a[1] = x; s[1] = song; }
-    } else {
-      a[2] = x; s[2] = song;
-    }
-  }
-};
-
-// Pass A over acc, songs i = tid + NT e: each song's approximation into the
-// thread's three best.
-template <int MODEL, int NT>
-__device__ __forceinline__ void cand_pass_a(const ScoreParams& p, const unsigned long long* acc,
-                                            const unsigned* heard, int blo, int bw, CandTop3& t) {
+template <int MODEL, int NT, int EMAX, bool PF>
+__device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsigned long long* acc,
+                                               const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
+                                               long long* ck, int* cs, int cap, long long* fk, int* fs,
+                                               long long* sb, const float (&rq)[EMAX]) {
+  constexpr int NG = NT / 16;
   const int tid = threadIdx.x;
+  float ap[EMAX];
+  long long mk = kKeyNone;
+  int ms = INT_MAX;
 #ifndef MR_CAND_EB
 #define MR_CAND_EB 4
 #endif
   constexpr int EB = MR_CAND_EB;  // songs per thread whose loads are issued together
-  for (int i0 = tid; i0 < bw; i0 += EB * NT) {
+#pragma unroll
+  for (int e0 = 0; e0 < EMAX; e0 += EB) {
     unsigned long long av[EB];
     float rv[EB];
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int i = i0 + j * NT;
+      const int i = tid + (e0 + j) * NT;
       av[j] = 0ull;
       rv[j] = 0.f;
-      if (i < bw) {
+      if (e0 + j < EMAX && i < bw) {
         av[j] = acc[i];
-        rv[j] = MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f;
+        // PF: loaded at the kernel's start, in flight during stage 2
+        rv[j] = MODEL != MR_IBM ? 1.f : PF ? rq[e0 + j < EMAX ? e0 + j : 0] : p.rsq_c[blo + i];
       }
     }
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int i = i0 + j * NT;
-      if (i < bw && !((heard[i >> 5] >> (i & 31)) & 1u)) t.insert(cand_approx(av[j], rv[j]), i);
+      const int e = e0 + j;
+      if (e >= EMAX) continue;
+      const int i = tid + e * NT;
+      float a = -1.f;
+      if (i < bw && !((heard[i >> 5] >> (i & 31)) & 1u)) {
+        const float hi = (float)(unsigned)(av[j] >> 32), lo = (float)(unsigned)av[j];
+        a = __fmaf_rn(hi, 4294967296.f, lo) * rv[j];
+        take_if_before(mk, ms, (long long)__float_as_uint(a), blo + i);
+      }
+      ap[e] = a;
     }
   }
-}
-
-// The selection of wide_cand_topk: tau over the threads' best
-// approximations, the survivors (approximation >= tau (1 - 2^-17)) with
-// their exact keys from the final accumulators, their ranks. A thread whose
-// third best survives may hold more survivors: it rescans its songs (songs
-// i = tid + NT e, or with `blocked` the dense pass's layout: DS consecutive
-// songs per thread per block of DS x NT).
-template <int MODEL, int NT, int DS>
-__device__ __forceinline__ bool cand_select(const ScoreParams& p, const unsigned long long* acc,
-                                            const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
-                                            long long* ck, int* cs, int cap, long long* fk, int* fs, long long* sb,
-                                            const CandTop3& t, bool blocked) {
-  constexpr int NG = NT / 16;
-  const int tid = threadIdx.x;
+  MR_STAMP(3);
+#if MR_CAND_STUB == 1
+  if (mk != -7) return false;
+#endif
   long long tk;
   int tsg;
-  block_tau<NT, NG>(k, t.a[0] >= 0.f ? (long long)__float_as_uint(t.a[0]) : kKeyNone,
-                    t.a[0] >= 0.f ? blo + t.s[0] : INT_MAX, gm, tk, tsg, sb);
+  block_tau<NT, NG>(k, mk, ms, gm, tk, tsg, sb);
+#if MR_CAND_STUB == 2
+  if (tk != -7) return false;
+#endif
   int* counter = reinterpret_cast<int*>(reinterpret_cast<long long*>(gm) + NG + 1) + NG + 1;
   int* crank = counter + 1 + NG;
   const float thr = __uint_as_float((unsigned)tk) * (1.f - 0x1p-17f);  // tk = 0 (none): every song
   const double inv_f = ldexp(1.0, -p.frac_bits);
-  auto emit = [&](int i) {
+  // the thread's survivors as a bit mask (heard / past the tile: a = -1), then
+  // a compact loop over the set bits (a few per tile: no unrolled 20-way body)
+  unsigned sm = 0u;
+#pragma unroll
+  for (int e = 0; e < EMAX; ++e) sm |= ap[e] >= thr ? 1u << e : 0u;
+  while (sm) {
+    const int e = __builtin_ctz(sm);
+    sm &= sm - 1u;
+    const int i = tid + e * NT;
     double score = (double)(long long)acc[i] * inv_f;
     if (MODEL == MR_IBM) score = score / p.sqrt_c[blo + i];
     const int pos = atomicAdd(counter, 1);
     if (pos < cap) { ck[pos] = __double_as_longlong(score); cs[pos] = blo + i; }
-  };
-  if (t.a[2] >= 0.f && t.a[2] >= thr) {  // maybe more than three: every song of the thread again
-    auto one = [&](int i) {
-      if ((heard[i >> 5] >> (i & 31)) & 1u) return;
-      if (cand_approx(acc[i], MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f) >= thr) emit(i);
-    };
-    if (blocked) {
-      for (int b0 = DS * tid; b0 < bw; b0 += DS * NT)
-        for (int j = 0; j < DS && b0 + j < bw; ++j) one(b0 + j);
-    } else {
-      for (int i = tid; i < bw; i += NT) one(i);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (t.a[j] >= 0.f && t.a[j] >= thr) emit(t.s[j]);
   }
   __syncthreads();
   stamp_at(sb, 11);
@@ -1883,6 +1850,13 @@ __device__ __forceinline__ bool cand_select(const ScoreParams& p, const unsigned
   rank_survivors<NT>(nc, k, ck, cs, crank, fk, fs);
   return true;
 }
+#ifndef MR_CAND_E
+#define MR_CAND_E 20
+#endif
+#ifndef MR_CAND_PF
+#define MR_CAND_PF 0  // 1: wide_cand_topk's scales loaded at the scoring kernel's start (C4 41.5 vs 41.1 ms)
+#endif
+constexpr int kCandE = MR_CAND_E;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
@@ -1940,12 +1914,17 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       scp[e] = i < bw ? p.sqrt_c[blo + i] : 1.0;
     }
   }
-  // candidate-only top-k (p.cand): the approximations of this thread's songs
-  // and its best, from the co-listening route's last dense pass (kFuseA:
-  // the dense pass's layout) or from pass A after stage 2
-  constexpr bool kFuseA = COOC;
-  CandTop3 ctop;
-  bool fused_a = false;
+  // candidate-only top-k: this thread's 1/sqrt(c) scales (songs tid + NT e)
+  // loaded now, in flight while stage 2 runs (4 B each, 20 registers)
+  constexpr bool kCPF = MR_CAND_PF && MODEL == MR_IBM && COOC;
+  float rq[kCandE];
+  if constexpr (kCPF) {
+#pragma unroll
+    for (int e = 0; e < kCandE; ++e) {
+      const int i = tid + e * NT;
+      rq[e] = p.cand && i < bw ? p.rsq_c[blo + i] : 0.f;
+    }
+  }
   // co-listening route: the first descriptor pass's row lookups (te_row /
   // te_songs, then seg_len / seg_off / q_song) issued around the zeroing and
   // the heard bitmap instead of after them (two dependent loads off the
@@ -2054,6 +2033,47 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       if (tid == 0) m_pre[ns] = total;
       __syncthreads();
       MR_STAMP(12);  // (the last descriptor pass's) descriptors ready
+      if (nd > 0) {
+        // DS songs per thread per block of DS * NT, every dense row summed in
+        // registers (DS = 8: one 8-B load per row; 16: one 16-B load per row,
+        // half the blocks per tile)
+        constexpr int DS = MR_COOC_DS;
+        typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
+        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
+          unsigned long long aa[DS];
+#pragma unroll
+          for (int i = 0; i < DS; ++i) aa[i] = 0ull;
+          // DU dense rows per step, their loads issued together
+          constexpr int DU = MR_COOC_DU;
+          for (int d0 = 0; d0 < nd; d0 += DU) {
+            dvec_t v0[DU];
+            unsigned long long qd[DU];
+#pragma unroll
+            for (int j = 0; j < DU; ++j) {
+              const int d = d0 + j;
+              qd[j] = 0ull;
+              v0[j] = dvec_t(0u);
+              if (d < nd) {
+                qd[j] = d_q[d];
+                v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + d_off[d] + (b0 >> 2));
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < DU; ++j) {
+#pragma unroll
+              for (int i = 0; i < DS; ++i) {
+                const unsigned c = (v0[j][i >> 2] >> (8 * (i & 3))) & 0xffu;
+                aa[i] += (unsigned long long)c * qd[j];
+              }
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < DS; ++i)
+            if (b0 + i < bw) acc[b0 + i] += aa[i];
+        }
+        __syncthreads();  // the sparse walk's atomics may hit any song
+      }
+      MR_STAMP(13);  // dense rows summed
       // 4 consecutive entries per thread and load (one 16-B load when they
       // lie in one segment, else entry by entry), U loads in flight
       constexpr int U = MR_COOC_U;
@@ -2096,80 +2116,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
             if (wq[j][i])
               atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
       }
-      MR_STAMP(13);  // sparse segments walked (this wave)
-      // DS songs per thread per block of DS * NT, every dense row summed in
-      // registers (DS = 8: one 8-B load per row; 16: one 16-B load per row,
-      // half the blocks per tile), after the sparse walk: the rows' counts
-      // then complete each song's accumulator in registers
-      constexpr int DS = MR_COOC_DS;
-      typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
-      auto dense_block = [&](int b0, unsigned long long (&aa)[DS]) {
-#pragma unroll
-        for (int i = 0; i < DS; ++i) aa[i] = 0ull;
-        // DU dense rows per step, their loads issued together
-        constexpr int DU = MR_COOC_DU;
-        for (int d0 = 0; d0 < nd; d0 += DU) {
-          dvec_t v0[DU];
-          unsigned long long qd[DU];
-#pragma unroll
-          for (int j = 0; j < DU; ++j) {
-            const int d = d0 + j;
-            qd[j] = 0ull;
-            v0[j] = dvec_t(0u);
-            if (d < nd) {
-              qd[j] = d_q[d];
-              v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + d_off[d] + (b0 >> 2));
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < DU; ++j) {
-#pragma unroll
-            for (int i = 0; i < DS; ++i) {
-              const unsigned c = (v0[j][i >> 2] >> (8 * (i & 3))) & 0xffu;
-              aa[i] += (unsigned long long)c * qd[j];
-            }
-          }
-        }
-      };
-      const bool last = c0 + p.nseg >= t1;
-      if constexpr (kFuseA) {
-        if (last && p.cand) {
-          // the last pass with the candidate-only top-k: every song's final
-          // accumulator is formed here (sparse entries in LDS + dense rows in
-          // registers), stored, and its fp32 approximation kept (pass A of
-          // wide_cand_topk, fused: no second pass over the tile)
-          __syncthreads();  // the sparse walk's atomics are in
-          for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
-            float rv[DS];  // (issued before the rows' loads: in flight together)
-#pragma unroll
-            for (int i = 0; i < DS; ++i) rv[i] = b0 + i < bw ? p.rsq_c[blo + b0 + i] : 0.f;
-            unsigned long long aa[DS];
-            dense_block(b0, aa);
-#pragma unroll
-            for (int i = 0; i < DS; ++i) {
-              const int s0 = b0 + i;
-              if (s0 < bw) {
-                const unsigned long long v = acc[s0] + aa[i];
-                acc[s0] = v;
-                if (!((heard[s0 >> 5] >> (s0 & 31)) & 1u)) ctop.insert(cand_approx(v, rv[i]), s0);
-              }
-            }
-          }
-          fused_a = true;
-        }
-      }
-      if (!fused_a && nd > 0) {
-        __syncthreads();  // the sparse walk's atomics may hit any song
-        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
-          unsigned long long aa[DS];
-          dense_block(b0, aa);
-#pragma unroll
-          for (int i = 0; i < DS; ++i)
-            if (b0 + i < bw) acc[b0 + i] += aa[i];
-        }
-      }
       __syncthreads();  // the next pass rewrites the descriptors
-      MR_STAMP(14);  // dense rows summed
+      MR_STAMP(14);  // sparse segments walked
     }
   } else {
   // stage 2: R neighbours per thread in flight; each segment's first kSeg
@@ -2204,7 +2152,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   int* fs = reinterpret_cast<int*>(smem_raw + L.fs);
   const int k = KS == 10 ? 10 : p.topk;
   // top-k-only runs: the candidate-only tile top-k (p.cand: no dense row, no
-  // min / max, 1 <= k <= NT / 16 — set by the host)
+  // min / max, 1 <= k <= NT / 16, bw <= kCandE * NT — set by the host)
   bool have = false;
 #ifdef MR_STAMPS
   long long* sbp = p.stamps ? p.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kStampSlots : nullptr;
@@ -2212,10 +2160,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   long long* sbp = nullptr;
 #endif
   if (p.cand) {
-    if (!fused_a) cand_pass_a<MODEL, NT>(p, acc, heard, blo, bw, ctop);
-    MR_STAMP(3);
-    have = cand_select<MODEL, NT, MR_COOC_DS>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws, min(256, NW * k),
-                                              fk, fs, sbp, ctop, fused_a);
+    have = wide_cand_topk<MODEL, NT, kCandE, kCPF>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
+                                                   min(256, NW * k), fk, fs, sbp, rq);
     MR_STAMP(6);
   }
   if (!have) {
@@ -4671,7 +4617,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   {  // the candidate-only tile top-k (wide_cand_topk): top-k-only wide runs
     const char* e = std::getenv("MR_WIDE_CAND");
     const int nt = route == 2 ? c->cooc_nt : kWideThreads;  // the scoring kernel's threads
-    c->cand_on = wide && !c->opt.dense && k >= 1 && k <= nt / 16 && !c->opt.topk_lists &&
+    c->cand_on = wide && !c->opt.dense && k >= 1 && k <= nt / 16 && !c->opt.topk_lists && bs <= kCandE * nt &&
                  !(e && e[0] == '0');
   }
   c->wide_lds = wide ? (size_t)wide_lds<kWideThreads>(bs, k, n_chunks).total : 0;

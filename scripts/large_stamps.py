@@ -50,8 +50,8 @@ span = end.max() - t0
 dur = end - rt[:, 0]
 print(f"{n_tr}/{n_te} {model}: tiles={tiles} WGs={live.sum()} kernel span {span / 1e3:.2f} ms; "
       f"sum(WG time)/256 = {dur.sum() / 256 / 1e3:.2f} ms")
-for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), (" cooc descr", 1, 12), (" cooc sparse", 12, 13),
-                   (" cooc dense", 13, 14), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5),
+for name, a, b in (("prefix", 0, 1), ("stage2", 1, 2), (" cooc descr", 1, 12), (" cooc dense", 12, 13),
+                   (" cooc sparse", 13, 14), ("epilogue", 2, 3), ("tile-topk", 3, 4), ("handoff", 4, 5),
                    (" topk scan", 3, 6), (" topk wave", 6, 7), (" topk barrier", 7, 8), (" topk merge", 8, 4),
                    (" thr pass1", 3, 9), (" thr rank", 9, 10), (" thr pass2", 10, 11), (" thr select", 11, 4)):
     d = rt[:, b] - rt[:, a]
