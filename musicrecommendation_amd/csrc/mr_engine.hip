@@ -1071,13 +1071,6 @@ struct ScoreParams {
   const long long* seg_off;      // [tile][row]: first pool entry of the row's tile segment
   const int* seg_len;            // [tile][row]: its entries
   const unsigned* pool;          // entries (tile-local song << kCoocCntBits) | C[s2][s]
-  // per (tile, te_songs entry): its row's segment in the tile (seg_off /
-  // seg_len gathered once per run by k_cooc_tdesc; 0 / 0 without a row), and
-  // per entry its ibm weight q_song (te_q): the scoring's descriptor loads
-  // one dependent level after te_off
-  const long long* tseg_off;
-  const int* tseg_len;
-  long long n_te_entries;
   // wide shape, dense output: ordered keys of each user's min / max stored
   // score ([user] min, [mm_n + user] max; mr_dense_minmax), or null
   unsigned long long* mm_key;
@@ -1937,16 +1930,14 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   // the heard bitmap instead of after them (two dependent loads off the
   // descriptor phase's critical path)
   constexpr bool kDPF = COOC && MR_COOC_DPF;
-  int pf_sl = 0;
+  int pf_r = -1, pf_s = 0, pf_sl = 0;
   long long pf_off = 0;
   unsigned long long pf_q = 0ull;
   if constexpr (kDPF) {
     const long long a = p.te_off[u];
     if (tid < min<long long>(p.nseg, p.te_off[u + 1] - a)) {
-      const size_t ix = (size_t)tile * p.n_te_entries + a + tid;
-      pf_sl = p.tseg_len[ix];
-      pf_off = p.tseg_off[ix];
-      pf_q = (unsigned long long)p.te_q[a + tid];
+      pf_r = p.te_row[a + tid];
+      pf_s = p.te_songs[a + tid];
     }
   }
 #if MR_WIDE_Z16  // 16-B stores: two songs per store (acc is 16-B aligned; bs is even)
@@ -1954,6 +1945,13 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 #else
   for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
 #endif
+  if constexpr (kDPF) {
+    if (pf_r >= 0) {
+      pf_sl = p.seg_len[(size_t)tile * p.n_rows + pf_r];
+      pf_off = p.seg_off[(size_t)tile * p.n_rows + pf_r];
+      pf_q = (unsigned long long)p.q_song[pf_s];
+    }
+  }
   for (int i = tid; i < bs / 32; i += NT) heard[i] = 0u;
   __syncthreads();
   for (long long i = p.te_off[u] + tid; i < p.te_off[u + 1]; i += NT) {
@@ -1990,31 +1988,37 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     int* m_pre = reinterpret_cast<int*>(d_q + p.nseg);
     int* d_fmt = m_pre + p.nseg + 1;
     const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
-    const int* slen = p.tseg_len + (size_t)tile * p.n_te_entries;
-    const long long* soff = p.tseg_off + (size_t)tile * p.n_te_entries;
+    const int* slen = p.seg_len + (size_t)tile * p.n_rows;
+    const long long* soff = p.seg_off + (size_t)tile * p.n_rows;
     for (long long c0 = t0; c0 < t1; c0 += p.nseg) {
       const int ns = (int)min<long long>(p.nseg, t1 - c0);
       int len = 0, isd = 0, fmt = 0;
       long long off = 0, tail_off = -1;
       unsigned long long q = 0ull;
       if (tid < ns) {
-        int sl;
+        int r, sl = 0;
         if (kDPF && c0 == t0) {  // (prefetched above)
+          r = pf_r;
           sl = pf_sl;
           off = pf_off;
           q = pf_q;
         } else {
-          sl = slen[c0 + tid];
-          off = soff[c0 + tid];
-          q = (unsigned long long)p.te_q[c0 + tid];
+          r = p.te_row[c0 + tid];
+          if (r >= 0) {
+            sl = slen[r];
+            off = soff[r];
+            q = (unsigned long long)p.q_song[p.te_songs[c0 + tid]];
+          }
         }
-        if (sl < 0) {  // saturated count bytes, then the excess entries
-          isd = 1;
-          fmt = sl;
-          len = kCoocDenseTail - sl;
-          tail_off = off + cooc_dense_words(bw);
-        } else {
-          len = sl;  // (0: no row, or no count in this tile)
+        if (r >= 0) {
+          if (sl < 0) {  // saturated count bytes, then the excess entries
+            isd = 1;
+            fmt = sl;
+            len = kCoocDenseTail - sl;
+            tail_off = off + cooc_dense_words(bw);
+          } else {
+            len = sl;
+          }
         }
       }
       int total, nd;
@@ -3271,25 +3275,6 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
   stamp_val(sb, 7, big ? 1 : p.n_grp);
 }
 
-// The scoring's per-(tile, te_songs entry) descriptors of a run: its row's
-// segment (seg_off / seg_len of the index just built), 0 / 0 without a row.
-__global__ __launch_bounds__(256) void k_cooc_tdesc(const int* te_row, long long nte, int n_rows,
-                                                    const long long* seg_off, const int* seg_len,
-                                                    long long* tseg_off, int* tseg_len) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nte) return;
-  const int t = blockIdx.y;
-  const int r = te_row[i];
-  long long off = 0;
-  int len = 0;
-  if (r >= 0) {
-    off = seg_off[(size_t)t * n_rows + r];
-    len = seg_len[(size_t)t * n_rows + r];
-  }
-  tseg_off[(size_t)t * nte + i] = off;
-  tseg_len[(size_t)t * nte + i] = len;
-}
-
 // The records of k_cooc_group, built once per load: one thread per train user
 // walks its sorted shard row and writes its base and the start of every tile.
 __global__ __launch_bounds__(256) void k_urec(const long long* sr_off, const unsigned* sr_songs, int n_tr, int n_tiles,
@@ -3563,7 +3548,6 @@ struct mr_ctx {
   int shape = kShapeSeparate;
   int last_model = -1;
   int n_tr = 0, n_te = 0, n_s = 0;
-  long long n_te_entries = 0;  // test-visible (user, song) entries: te_off[n_te]
   int song_lo = 0, song_hi = 0, width = 0;
   int block_songs = 0, n_tiles = 0;
   int cap = 0, batch = 0;
@@ -3618,8 +3602,6 @@ struct mr_ctx {
   size_t cooc_lds = 0;
   ScoreKernel cooc_kernel = nullptr;
   DevBuf<int> row_song, te_row, seg_len;
-  DevBuf<long long> tseg_off;      // scoring descriptors per (tile, te_songs entry), k_cooc_tdesc
-  DevBuf<int> tseg_len;
   DevBuf<long long> row_base, seg_off;
   DevBuf<unsigned> pool;
   DevBuf<unsigned> row_nnz;        // per run: each index row's non-zeros over the shard
@@ -3661,7 +3643,6 @@ struct mr_ctx {
     stamps.release();
     flag.release();
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
-    tseg_off.release(); tseg_len.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     urec.release(); lrec.release(); rdesc.release(); grp = n_grp = urec_words = lrec_words = 0;
@@ -4540,14 +4521,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     if ((rc = dev_alloc(c->seg_off, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->seg_len, nr * n_tiles))) return rc;
     if ((rc = dev_alloc(c->pool, (size_t)pool_cap))) return rc;
-    {  // the scoring's descriptors: per entry its ibm weight, per (tile, entry) its segment
-      const size_t nte = std::max<size_t>(1, (size_t)d->te_off[n_te]);
-      std::vector<long long> tq(nte, 0);
-      for (size_t i = 0; i < (size_t)d->te_off[n_te]; ++i) tq[i] = q_song[d->te_songs[i]];
-      if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
-      if ((rc = dev_alloc(c->tseg_off, nte * n_tiles))) return rc;
-      if ((rc = dev_alloc(c->tseg_len, nte * n_tiles))) return rc;
-    }
     // heavy rows, then light rows with large tables, then the small-table ones
     std::stable_sort(light_rows.begin(), light_rows.end(), [&](int32_t x, int32_t y) {
       return light_tier(row_slots[x] & kLightSlotsMask, n_tiles) < light_tier(row_slots[y] & kLightSlotsMask, n_tiles);
@@ -4731,7 +4704,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   trace("upload");
 
   c->n_tr = n_tr; c->n_te = n_te; c->n_s = n_s;
-  c->n_te_entries = (long long)d->te_off[n_te];
   c->song_lo = lo; c->song_hi = hi; c->width = width;
   c->block_songs = bs; c->n_tiles = n_tiles;
   c->cap = cap; c->batch = batch;
@@ -4986,12 +4958,6 @@ int run_cooc(mr_ctx* c) {
         MR_HIP(hipStreamWaitEvent(st, c->side_join[i], 0));
       }
   }
-  const long long nte_all = c->n_te_entries;
-  if (nte_all > 0) {  // the scoring's descriptors of this run's index
-    hipLaunchKernelGGL(k_cooc_tdesc, dim3((unsigned)((nte_all + 255) / 256), c->n_tiles), dim3(256), 0, st,
-                       c->te_row.p, nte_all, c->n_rows, c->seg_off.p, c->seg_len.p, c->tseg_off.p, c->tseg_len.p);
-    MR_HIP(hipGetLastError());
-  }
   if (timed) MR_HIP(hipEventRecord(ev[1], st));
   for (int y0 = 0; y0 < c->n_te; y0 += 65528) {
     const int ny = std::min(65528, c->n_te - y0);
@@ -5009,8 +4975,6 @@ int run_cooc(mr_ctx* c) {
     sp.sqrt_c = c->sqrt_c.p; sp.q_song = c->q_song.p;
     sp.n_rows = c->n_rows; sp.nseg = c->nseg;
     sp.te_row = c->te_row.p; sp.seg_off = c->seg_off.p; sp.seg_len = c->seg_len.p; sp.pool = c->pool.p;
-    sp.tseg_off = c->tseg_off.p; sp.tseg_len = c->tseg_len.p; sp.n_te_entries = c->n_te_entries;
-    sp.te_q = c->te_q.p;
     sp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p;
     sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
     sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
