@@ -2334,6 +2334,11 @@ struct CoocParams {
   // row's first record at rdesc.z (built at load by k_lrec from urec)
   const unsigned* lrec;
   int lrec_words;
+  // k_cooc_light*: per (light row, listener) the listener's shard-row range
+  // [a, b) of sr_songs as two u32, in the row's order, the row's first at
+  // rdesc.z (built at load by k_llrec): one 8-B load instead of the listener
+  // id and then its two sr_off words
+  const unsigned* llrec;
   long long* lstamps;            // diagnostic build: [light row of the launch][8] (k_cooc_light*)
   // k_cooc_light* / k_cooc_group: the launch's rows as {row, row_slots value,
   // first listener in trs_users, listeners} (one load instead of rows ->
@@ -2748,13 +2753,13 @@ __device__ __forceinline__ void light_insert_queue(unsigned* tab, unsigned mask,
 
 // range of rows_walk: listener v's whole shard row
 struct ShardRow {
-  const long long* off;
-  __device__ __forceinline__ void operator()(int v, long long& a, long long& b) const {
-    a = off[v];
-    b = off[v + 1];
+  const unsigned* rec;  // the row's first (a, b) record
+  __device__ __forceinline__ void operator()(int x, long long& a, long long& b) const {
+    const uint2 r = reinterpret_cast<const uint2*>(rec)[x];
+    a = r.x;
+    b = r.y;
   }
 };
-__device__ __forceinline__ ShardRow shard_row(const CoocParams& p) { return ShardRow{p.sr_off}; }
 
 // Light index rows: one workgroup per row (instead of one per (row, tile)).
 // The row's listeners' whole shard rows (sr_off / sr_songs) are walked by
@@ -2781,10 +2786,10 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   for (int i = tid; 4 * i < S; i += NT) reinterpret_cast<uint4*>(tab)[i] = make_uint4(0u, 0u, 0u, 0u);  // (S: a power of 2 >= 1024)
   for (int i = tid; i < p.n_tiles; i += NT) { tcnt[i] = 0; tpos[i] = 0; }
   const int n = rd.w;
-  const int* lst = p.trs_users + (unsigned)rd.z;
+  const unsigned* lst = p.llrec + 2 * (size_t)(unsigned)rd.z;  // the row's listeners' ranges
   __syncthreads();  // the table and the tile counters are zero
   stamp_rt(sb, 1);
-  rows_walk(tid, NT, rd.y >> kLightGlogShift, [&](int l) { return lst[l]; }, n, shard_row(p), p.sr_songs,
+  rows_walk(tid, NT, rd.y >> kLightGlogShift, [](int l) { return l; }, n, ShardRow{lst}, p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   __syncthreads();
   stamp_rt(sb, 2);
@@ -2859,10 +2864,10 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   for (int i = lane; 4 * i < S; i += 64) reinterpret_cast<uint4*>(tab)[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int i = lane; i < p.n_tiles; i += 64) { tcnt[i] = 0; tpos[i] = 0; }
   const int n = rd.w;
-  const int* lst = p.trs_users + (unsigned)rd.z;
+  const unsigned* lst = p.llrec + 2 * (size_t)(unsigned)rd.z;  // the row's listeners' ranges
   wave_lds_sync();  // the table and the tile counters are zero
   stamp_rt_wave(sb, 1);
-  rows_walk(lane, 64, rd.y >> kLightGlogShift, [&](int l) { return lst[l]; }, n, shard_row(p), p.sr_songs,
+  rows_walk(lane, 64, rd.y >> kLightGlogShift, [](int l) { return l; }, n, ShardRow{lst}, p.sr_songs,
             [&](const unsigned (&k)[8], int m) { light_insert_queue(tab, mask, sh, k, m); });
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
@@ -3311,6 +3316,18 @@ __global__ __launch_bounds__(256) void k_lrec(const int4* rdesc, const int* row_
   }
 }
 
+// The light rows' per-(row, listener) shard-row ranges, built once per load:
+// one workgroup per light row (rd.z: its first record, rd.w: its listeners).
+__global__ __launch_bounds__(256) void k_llrec(const int4* rdesc, const int* row_song, const long long* trs_off,
+                                               const int* trs_users, const long long* sr_off, uint2* llrec) {
+  const int4 rd = rdesc[blockIdx.x];
+  const long long s0 = trs_off[row_song[rd.x]];
+  for (int l = threadIdx.x; l < rd.w; l += 256) {
+    const int v = trs_users[s0 + l];
+    llrec[(size_t)(unsigned)rd.z + l] = make_uint2((unsigned)sr_off[v], (unsigned)sr_off[v + 1]);
+  }
+}
+
 // Light-row tier t (light_tier_slots): its table size and workgroup width
 // fixed at compile time. light_tier_call(t, stream, n, &params, ..) launches
 // n rows; with params == nullptr it sets the kernel's LDS attribute instead.
@@ -3627,6 +3644,7 @@ struct mr_ctx {
   DevBuf<unsigned> sr_songs;
   DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts (load-time only: lrec's source)
   DevBuf<unsigned> lrec;           // k_cooc_group: per-(row, listener) base + tile-group starts
+  DevBuf<uint2> llrec;             // k_cooc_light*: per-(row, listener) shard-row ranges
   int grp = 0, n_grp = 0, urec_words = 0, lrec_words = 0;
   int group_nt = 1024;             // threads per k_cooc_group workgroup (MR_COOC_GNT)
 
@@ -3645,7 +3663,7 @@ struct mr_ctx {
     row_song.release(); te_row.release(); seg_len.release(); row_base.release(); seg_off.release();
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
-    urec.release(); lrec.release(); rdesc.release(); grp = n_grp = urec_words = lrec_words = 0;
+    urec.release(); lrec.release(); llrec.release(); rdesc.release(); grp = n_grp = urec_words = lrec_words = 0;
     row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
@@ -4528,7 +4546,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     std::vector<int32_t> order(heavy_rows);
     order.insert(order.end(), light_rows.begin(), light_rows.end());
     if ((rc = dev_upload(c->rows_order, order.data(), order.size(), st))) return rc;
-    int64_t n_lrec = 0;  // k_cooc_group's records: the u16 heavy rows' listeners
+    int64_t n_lrec = 0;   // k_cooc_group's records: the u16 heavy rows' listeners
+    int64_t n_llrec = 0;  // k_cooc_light*'s records: the light rows' listeners
     {
       std::vector<int4> rd(std::max<size_t>(1, order.size()));
       for (size_t i = 0; i < order.size(); ++i) {
@@ -4538,6 +4557,9 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         if (grp > 0 && (int)i >= n_heavy32 && i < heavy_rows.size()) {  // the first record in lrec
           z = (int)n_lrec;
           n_lrec += cnt;
+        } else if (i >= heavy_rows.size()) {  // a light row: its first range record in llrec
+          z = (int)n_llrec;
+          n_llrec += cnt;
         }
         rd[i] = make_int4(r, row_slots[r], z, cnt);
       }
@@ -4568,6 +4590,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       });
       if ((rc = dev_upload(c->sr_off, reinterpret_cast<const long long*>(so.data()), so.size(), st))) return rc;
       if ((rc = dev_upload(c->sr_songs, ss.data(), ss.size(), st))) return rc;
+      if (!light_rows.empty()) {  // the light rows' listener ranges
+        if ((rc = dev_alloc(c->llrec, (size_t)std::max<int64_t>(1, n_llrec)))) return rc;
+        hipLaunchKernelGGL(k_llrec, dim3((unsigned)light_rows.size()), dim3(256), 0, st,
+                           c->rdesc.p + heavy_rows.size(), c->row_song.p, c->trs_off.p, c->trs_users.p, c->sr_off.p,
+                           c->llrec.p);
+        MR_HIP(hipGetLastError());
+      }
       if (grp > 0) {  // k_cooc_group's records, on the device: per user (tile starts), then per (row, listener)
         if ((rc = dev_alloc(c->urec, (size_t)std::max(1, n_tr) * urec_words))) return rc;
         hipLaunchKernelGGL(k_urec, dim3((std::max(1, n_tr) + 255) / 256), dim3(256), 0, st, c->sr_off.p,
@@ -4947,6 +4976,7 @@ int run_cooc(mr_ctx* c) {
       CoocParams lp = cp;
       lp.rows = c->rows_order.p + lr;
       lp.rdesc = c->rdesc.p + lr;
+      lp.llrec = reinterpret_cast<const unsigned*>(c->llrec.p);
       lp.lstamps = c->stamps.p ? c->stamps.p + c->lstamp_off + (size_t)(lr - c->n_heavy) * 8 : nullptr;
       hipStream_t ls = side ? c->side[t < 2 ? 0 : 1] : st;
       if (int rc2 = light_tier_call(t, ls, c->n_light_tier[t], &lp, lp)) return rc2;
