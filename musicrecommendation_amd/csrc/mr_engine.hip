@@ -2021,9 +2021,12 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
           }
         }
       }
-      int total, nd;
-      const int pre = block_excl_scan_nt<NT>(len, &total, s_scan);
-      const int dpre = block_excl_scan_nt<NT>(isd, &nd, s_scan);
+      // one scan of (entries << 8 | dense): nseg <= 255 rows of < 32768
+      // entries each per pass (mr_load), so both sums fit
+      int tot_pk;
+      const int pk = block_excl_scan_nt<NT>((len << 8) | isd, &tot_pk, s_scan);
+      const int pre = pk >> 8, dpre = pk & 255;
+      const int total = tot_pk >> 8, nd = tot_pk & 255;
       if (tid < ns) {
         m_off[tid] = (tail_off >= 0 ? tail_off : off) - pre;
         m_q[tid] = q;
@@ -4671,7 +4674,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     const WideLds<kWideThreads> WL = c->cooc_nt == 512 ? wide_lds<512>(bs, k, n_chunks).as_wide()
                                                        : wide_lds<kWideThreads>(bs, k, n_chunks);
     c->cooc_score_lds = (size_t)WL.total;
-    c->nseg = std::min(c->cooc_nt, (WL.total - WL.wk - 8) / 40);
+    // (<= 255 per pass: the scoring packs a pass's entry and dense-row prefix sums in one int)
+    c->nseg = std::min(std::min(c->cooc_nt, (WL.total - WL.wk - 8) / 40), 255);
     if (c->nseg < 16) return fail(MR_E_INVALID, "co-listening route: no LDS for row descriptors");
     c->cooc_lds = (size_t)cooc_build_lds<false>(bs);
     c->n_heavy = (int)heavy_rows.size();
