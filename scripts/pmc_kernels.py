@@ -8,7 +8,7 @@ import re
 import sys
 from collections import defaultdict
 
-LOAD = ("k_urec", "k_sbound", "k_lrec")
+LOAD = ("k_urec", "k_sbound", "k_lrec", "k_llrec")
 
 
 def sums(d, counters):
