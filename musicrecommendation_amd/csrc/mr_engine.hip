@@ -1621,9 +1621,6 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_DS
 #define MR_COOC_DS 8        // co-listening route: dense-pass songs per thread per block (8 or 16)
 #endif
-#ifndef MR_COOC_DB
-#define MR_COOC_DB 2        // co-listening route: dense-pass blocks per thread whose row loads are issued together
-#endif
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
@@ -2045,55 +2042,37 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         // half the blocks per tile)
         constexpr int DS = MR_COOC_DS;
         typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
-        // DB blocks per thread per step, all their rows' loads issued
-        // together (a tile of 19,456 songs is 2.4 blocks of 8 x 1024: one
-        // memory round trip per step, not per block)
-        constexpr int DB = MR_COOC_DB;
-        for (int b0 = DS * tid; b0 < bw; b0 += DB * DS * NT) {
-          unsigned long long aa[DB][DS];
+        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
+          unsigned long long aa[DS];
 #pragma unroll
-          for (int b = 0; b < DB; ++b)
-#pragma unroll
-            for (int i = 0; i < DS; ++i) aa[b][i] = 0ull;
+          for (int i = 0; i < DS; ++i) aa[i] = 0ull;
           // DU dense rows per step, their loads issued together
           constexpr int DU = MR_COOC_DU;
           for (int d0 = 0; d0 < nd; d0 += DU) {
-            dvec_t v0[DB][DU];
+            dvec_t v0[DU];
             unsigned long long qd[DU];
 #pragma unroll
             for (int j = 0; j < DU; ++j) {
               const int d = d0 + j;
               qd[j] = 0ull;
-#pragma unroll
-              for (int b = 0; b < DB; ++b) v0[b][j] = dvec_t(0u);
+              v0[j] = dvec_t(0u);
               if (d < nd) {
                 qd[j] = d_q[d];
-                const long long od = d_off[d];
-#pragma unroll
-                for (int b = 0; b < DB; ++b) {
-                  const int bb = b0 + b * DS * NT;
-                  if (bb < bw) v0[b][j] = *reinterpret_cast<const dvec_t*>(p.pool + od + (bb >> 2));
-                }
+                v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + d_off[d] + (b0 >> 2));
               }
             }
 #pragma unroll
-            for (int b = 0; b < DB; ++b)
+            for (int j = 0; j < DU; ++j) {
 #pragma unroll
-              for (int j = 0; j < DU; ++j) {
-#pragma unroll
-                for (int i = 0; i < DS; ++i) {
-                  const unsigned c = (v0[b][j][i >> 2] >> (8 * (i & 3))) & 0xffu;
-                  aa[b][i] += (unsigned long long)c * qd[j];
-                }
+              for (int i = 0; i < DS; ++i) {
+                const unsigned c = (v0[j][i >> 2] >> (8 * (i & 3))) & 0xffu;
+                aa[i] += (unsigned long long)c * qd[j];
               }
+            }
           }
 #pragma unroll
-          for (int b = 0; b < DB; ++b) {
-            const int bb = b0 + b * DS * NT;
-#pragma unroll
-            for (int i = 0; i < DS; ++i)
-              if (bb + i < bw) acc[bb + i] += aa[b][i];
-          }
+          for (int i = 0; i < DS; ++i)
+            if (b0 + i < bw) acc[b0 + i] += aa[i];
         }
         __syncthreads();  // the sparse walk's atomics may hit any song
       }
