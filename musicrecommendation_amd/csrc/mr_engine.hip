@@ -2326,15 +2326,12 @@ struct CoocParams {
   int n_big;                     // k_cooc_build: the first n_big rows of the launch one workgroup per
                                  //   (row, tile), each tile's segment at row_base + tile * tcap
   int tcap;                      //   (words per tile of those rows); the rest one workgroup per row
-  // k_cooc_group: per train user a record of urec_words u32 words — word 0 the
-  // user's first entry in sr_songs, then u16 starts (relative to it) of every
-  // tile's entries, tiles 0..n_tiles — and the tile groups (grp tiles each)
-  const unsigned* urec;
-  int urec_words, grp, n_grp;
-  // k_cooc_group: per (row, listener) a record of lrec_words u32 words — word
-  // 0 the listener's first entry in sr_songs, then u16 starts (relative to
-  // it) of every tile group g = 0..n_grp — in the row's listener order, the
-  // row's first record at rdesc.z (built at load by k_lrec from urec)
+  // k_cooc_group: the tile groups (grp tiles each), and per (row, listener) a
+  // record of lrec_words u32 words — word 0 the listener's first entry in
+  // sr_songs, then u16 starts (relative to it) of every tile group g =
+  // 0..n_grp — in the row's listener order, the row's first record at rdesc.z
+  // (built at load by k_lrec from the per-user records of k_urec)
+  int grp, n_grp;
   const unsigned* lrec;
   int lrec_words;
   // k_cooc_light*: per (light row, listener) the listener's shard-row range
@@ -2917,8 +2914,11 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
 // grp tiles' u16 counters (two per LDS word) side by side in LDS, so one walk
 // of the row's listeners serves grp tiles. Each listener's entries of the
 // group are one contiguous run of its shard row (user-major sr_songs: the
-// songs ascend, so tiles do), found through the listener's record (urec: one
-// aligned line holds its base and every tile's start). k_cooc_build's walk
+// songs ascend, so tiles do), found through the (row, listener) record (lrec:
+// 16 contiguous bytes per listener of the row hold its base and every group's
+// start; round 4 read a listener id and then a per-user record line, 10 GB of
+// lines per C4 step for ~0.1 GB used, profiles/r05/group_lines_c4.json).
+// k_cooc_build's walk
 // gathered, per (row, tile, listener), a toff pair and a tile segment from two
 // tile-major arrays: two whole lines for ~5 entries, 20 times per listener at
 // C4 (107 GB of fetches per step for ~6 GB of entries).
