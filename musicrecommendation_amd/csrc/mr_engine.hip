@@ -1772,11 +1772,11 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
 // approximations (same acc, same c). Returns false, uniformly, when the
 // survivors overflow cap (e.g. fewer than k positive scores: tau = 0); acc
 // is untouched, so the caller then runs the all-songs path.
-template <int MODEL, int NT, int EMAX, bool PF>
+template <int MODEL, int NT, int EMAX>
 __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsigned long long* acc,
                                                const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
                                                long long* ck, int* cs, int cap, long long* fk, int* fs,
-                                               long long* sb, const float (&rq)[EMAX]) {
+                                               long long* sb) {
   constexpr int NG = NT / 16;
   const int tid = threadIdx.x;
   float ap[EMAX];
@@ -1785,7 +1785,7 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
 #ifndef MR_CAND_EB
 #define MR_CAND_EB 4
 #endif
-  constexpr int EB = MR_CAND_EB;  // songs per thread whose loads are issued together
+  constexpr int EB = MR_CAND_EB;  // songs per thread whose loads are issued together (10 spilled)
 #pragma unroll
   for (int e0 = 0; e0 < EMAX; e0 += EB) {
     unsigned long long av[EB];
@@ -1797,8 +1797,9 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
       rv[j] = 0.f;
       if (e0 + j < EMAX && i < bw) {
         av[j] = acc[i];
-        // PF: loaded at the kernel's start, in flight during stage 2
-        rv[j] = MODEL != MR_IBM ? 1.f : PF ? rq[e0 + j < EMAX ? e0 + j : 0] : p.rsq_c[blo + i];
+        // (loading these at the kernel's start, in flight during stage 2, ran
+        // 41.46 vs 41.08 ms at C4: profiles/r05/s2)
+        rv[j] = MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f;
       }
     }
 #pragma unroll
@@ -1816,15 +1817,9 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
     }
   }
   MR_STAMP(3);
-#if MR_CAND_STUB == 1
-  if (mk != -7) return false;
-#endif
   long long tk;
   int tsg;
   block_tau<NT, NG>(k, mk, ms, gm, tk, tsg, sb);
-#if MR_CAND_STUB == 2
-  if (tk != -7) return false;
-#endif
   int* counter = reinterpret_cast<int*>(reinterpret_cast<long long*>(gm) + NG + 1) + NG + 1;
   int* crank = counter + 1 + NG;
   const float thr = __uint_as_float((unsigned)tk) * (1.f - 0x1p-17f);  // tk = 0 (none): every song
@@ -1850,13 +1845,7 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
   rank_survivors<NT>(nc, k, ck, cs, crank, fk, fs);
   return true;
 }
-#ifndef MR_CAND_E
-#define MR_CAND_E 20
-#endif
-#ifndef MR_CAND_PF
-#define MR_CAND_PF 0  // 1: wide_cand_topk's scales loaded at the scoring kernel's start (C4 41.5 vs 41.1 ms)
-#endif
-constexpr int kCandE = MR_CAND_E;  // wide_cand_topk: songs per thread (tiles <= 20 x 1024 songs)
+constexpr int kCandE = 20;  // wide_cand_topk: songs per thread (tiles <= 20 x NT songs)
 
 // KS: register slots of the per-thread lists (10: k = 10 exactly, the
 // default, compiled in; 16: any k <= 16 at run time).
@@ -1912,17 +1901,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
     for (int e = 0; e < PF; ++e) {
       const int i = tid + e * NT;
       scp[e] = i < bw ? p.sqrt_c[blo + i] : 1.0;
-    }
-  }
-  // candidate-only top-k: this thread's 1/sqrt(c) scales (songs tid + NT e)
-  // loaded now, in flight while stage 2 runs (4 B each, 20 registers)
-  constexpr bool kCPF = MR_CAND_PF && MODEL == MR_IBM && COOC;
-  float rq[kCandE];
-  if constexpr (kCPF) {
-#pragma unroll
-    for (int e = 0; e < kCandE; ++e) {
-      const int i = tid + e * NT;
-      rq[e] = p.cand && i < bw ? p.rsq_c[blo + i] : 0.f;
     }
   }
   // co-listening route: the first descriptor pass's row lookups (te_row /
@@ -2163,8 +2141,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   long long* sbp = nullptr;
 #endif
   if (p.cand) {
-    have = wide_cand_topk<MODEL, NT, kCandE, kCPF>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
-                                                   min(256, NW * k), fk, fs, sbp, rq);
+    have = wide_cand_topk<MODEL, NT, kCandE>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
+                                             min(256, NW * k), fk, fs, sbp);
     MR_STAMP(6);
   }
   if (!have) {
