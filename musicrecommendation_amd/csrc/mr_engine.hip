@@ -1658,7 +1658,21 @@ constexpr int kCoocCntBits = 17;
 // of the same index may differ byte for byte; every consumer sums the entries
 // (order-free integer adds), so the scores never do. Compare indexes as sets.
 constexpr int kCoocDenseTail = -3;
-__host__ __device__ inline int cooc_dense_words(int bw) { return ((bw + 3) / 4 + 3) & ~3; }
+// Count-byte order of a dense segment: lane-interleaved blocks of 64 x DS
+// songs (DS = MR_COOC_DS). In each block, the DS-byte chunk t holds songs t,
+// t + 64, ..., t + 64 (DS - 1) of the block: the scoring's dense pass loads
+// chunk t in lane t (coalesced, as before) and adds its DS sums into acc at
+// songs t + 64 i — consecutive across the wave, so the LDS read-modify-writes
+// are free of bank conflicts (song-ordered chunks put the lanes' u64 adds
+// 8 x DS bytes apart: 16-way conflicts at DS = 8). The segment holds whole
+// blocks (songs past the tile: count 0).
+constexpr int kDenseDS = MR_COOC_DS;
+constexpr int kDenseBlock = 64 * kDenseDS;
+__host__ __device__ inline int cooc_dense_words(int bw) {
+  return (bw + kDenseBlock - 1) / kDenseBlock * (kDenseBlock / 4);
+}
+// the song of byte i of chunk c
+__host__ __device__ inline int cooc_dense_song(int c, int i) { return (c >> 6) * kDenseBlock + 64 * i + (c & 63); }
 constexpr int kCoocDenseDiv = 3;
 #ifndef MR_COOC_BIG_ROW
 #define MR_COOC_BIG_ROW 2048  // C4 44.74 vs 45.16 ms at 4096, 8x1 6.06 vs 6.10 (profiles/r04/s43, s44)
@@ -2018,9 +2032,10 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         // DS songs per thread per block of DS * NT, every dense row summed in
         // registers (DS = 8: one 8-B load per row; 16: one 16-B load per row,
         // half the blocks per tile)
-        constexpr int DS = MR_COOC_DS;
+        constexpr int DS = kDenseDS;
         typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
-        for (int b0 = DS * tid; b0 < bw; b0 += DS * NT) {
+        // chunk c = b0 / DS: songs cooc_dense_song(c, i) (wave-uniform block)
+        for (int b0 = DS * tid; (b0 & ~(kDenseBlock - 1)) < bw; b0 += DS * NT) {
           unsigned long long aa[DS];
 #pragma unroll
           for (int i = 0; i < DS; ++i) aa[i] = 0ull;
@@ -2049,8 +2064,10 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
             }
           }
 #pragma unroll
-          for (int i = 0; i < DS; ++i)
-            if (b0 + i < bw) acc[b0 + i] += aa[i];
+          for (int i = 0; i < DS; ++i) {
+            const int col = cooc_dense_song(b0 / DS, i);
+            if (col < bw) acc[col] += aa[i];
+          }
         }
         __syncthreads();  // the sparse walk's atomics may hit any song
       }
@@ -2378,6 +2395,44 @@ __host__ __device__ constexpr int cooc_light_lds() {
   return LightLds<NT, SMAX>::total;
 }
 
+// A dense segment's count bytes (cooc_dense_song order, saturated at sat)
+// at out[0, dwords), the excess (count - sat) of larger counts as entries
+// from out[dwords] on (*tail: their LDS counter). Lanes read consecutive
+// songs' counters and store consecutive chunks (CHUNK) or words.
+template <int NT, bool CHUNK, typename CountOf>
+__device__ __forceinline__ void cooc_write_dense(unsigned* out, int bw, int dwords, unsigned sat, int* tail,
+                                                 CountOf&& count_of) {
+  constexpr int WPC = kDenseDS / 4;  // words per chunk
+  if constexpr (CHUNK) {  // a whole chunk per thread, one store (k_cooc_group: 17.85 vs 18.27 ms at C4)
+    typedef unsigned chunk_t __attribute__((ext_vector_type(WPC)));
+    for (int c = threadIdx.x; c < dwords / WPC; c += NT) {
+      chunk_t v = chunk_t(0u);
+#pragma unroll
+      for (int i = 0; i < kDenseDS; ++i) {
+        const int col = cooc_dense_song(c, i);
+        const unsigned n = col < bw ? count_of(col) : 0u;
+        v[i >> 2] |= min(n, sat) << (8 * (i & 3));
+        if (n > sat) out[dwords + atomicAdd(tail, 1)] = ((unsigned)col << kCoocCntBits) | (n - sat);
+      }
+      reinterpret_cast<chunk_t*>(out)[c] = v;
+    }
+    return;
+  }
+  // a word per thread (k_cooc_build: the chunk's registers spilled, 1.04 vs 0.71 ms)
+  for (int x = threadIdx.x; x < dwords; x += NT) {  // word x: bytes 4 (x % WPC) .. +3 of chunk x / WPC
+    const int c = x / WPC, i0 = 4 * (x % WPC);
+    unsigned wv = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cooc_dense_song(c, i0 + j);
+      const unsigned n = col < bw ? count_of(col) : 0u;
+      wv |= min(n, sat) << (8 * j);
+      if (n > sat) out[dwords + atomicAdd(tail, 1)] = ((unsigned)col << kCoocCntBits) | (n - sat);
+    }
+    out[x] = wv;
+  }
+}
+
 // One finished tile of an index row (counters in LDS, count_of(i) = song i's
 // count, `total` non-zeros, the first `cap` of them listed in `touched`)
 // written at pool[off]: a dense segment (a count byte per song, saturated at
@@ -2404,17 +2459,7 @@ __device__ __forceinline__ int cooc_emit_tile(const CoocParams& p, int r, int ti
       // every song's count as a byte saturated at sat (255), the excess
       // (count - sat) of the few larger counts as sparse entries after them
       // (own counter: s_nz is still being read for `total` by other waves)
-      for (int i = tid; 4 * i < bw; i += NT) {
-        unsigned wv = 0u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = 4 * i + j;
-          const unsigned c = col < bw ? count_of(col) : 0u;
-          wv |= min(c, p.sat) << (8 * j);
-          if (c > p.sat) out[dwords + atomicAdd(s_tail, 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
-        }
-        out[i] = wv;
-      }
+      cooc_write_dense<NT, false>(out, bw, dwords, p.sat, s_tail, count_of);
       __syncthreads();
       const int tail = *s_tail;
       words = (dwords + tail + 3) & ~3;
@@ -2976,17 +3021,8 @@ __device__ __forceinline__ void cooc_emit_group16(const CoocParams& p, int r, bo
     const unsigned* cw = cnt + (size_t)k * (bs >> 1);
     unsigned* out = p.pool + seg;
     if (dense) {
-      for (int i = tid; 4 * i < bw; i += NT) {
-        unsigned wv = 0u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = 4 * i + j;
-          const unsigned c = col < bw ? (cw[col >> 1] >> ((col & 1) << 4)) & 0xffffu : 0u;
-          wv |= min(c, p.sat) << (8 * j);
-          if (c > p.sat) out[dwords + atomicAdd(&s_tail[k], 1)] = ((unsigned)col << kCoocCntBits) | (c - p.sat);
-        }
-        out[i] = wv;
-      }
+      cooc_write_dense<NT, true>(out, bw, dwords, p.sat, &s_tail[k],
+                           [&](int col) { return (cw[col >> 1] >> ((col & 1) << 4)) & 0xffffu; });
     } else {
       const uint4* cv = reinterpret_cast<const uint4*>(cw);
       const int nch = (bw + 7) >> 3;
@@ -4376,6 +4412,13 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         narrow = cooc_group_lds(bs, n_tiles) <= kLdsBytes;
       const int64_t lload = cooc_light_load_opt(), light_slots_max = cooc_light_max_opt(narrow);
       dense_div = cooc_dense_div_opt();
+      // a dense segment holds whole interleaved blocks (cooc_dense_words):
+      // the words past its songs' bytes, over every tile, on each heavy row's bound
+      int64_t dense_pad = 0;
+      for (int t = 0; t < n_tiles; ++t) {
+        const int bw = (int)(std::min<int64_t>(width, (int64_t)(t + 1) * bs) - (int64_t)t * bs);
+        dense_pad += cooc_dense_words(bw) - (bw + 3) / 4;
+      }
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
         if (light_ok && row_base[r] * 100 <= light_slots_max * lload && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
@@ -4398,7 +4441,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
           // (dense: count bytes <= kCoocDenseDiv / 4 x the non-zeros, + excess entries <= the non-zeros)
           const int64_t nz = row_base[r];
           const int64_t dn = std::max<int64_t>(1, std::min<int64_t>(dense_div, width)) * nz;
-          row_base[r] = ((std::min<int64_t>(width, dn) + nz + 3) & ~(int64_t)3) + 8 * (int64_t)n_tiles;
+          row_base[r] = ((std::min<int64_t>(width, dn) + nz + 3) & ~(int64_t)3) + 8 * (int64_t)n_tiles + dense_pad;
           heavy_rows.push_back((int32_t)r);
         }
       }
