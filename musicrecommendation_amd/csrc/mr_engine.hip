@@ -1621,6 +1621,9 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_DS
 #define MR_COOC_DS 8        // co-listening route: dense-pass songs per thread per block (8 or 16)
 #endif
+#ifndef MR_COOC_SPLIT
+#define MR_COOC_SPLIT 1     // co-listening scoring: the dense pass's u32 half-weight sums (frac_bits <= 32)
+#endif
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
@@ -1786,20 +1789,23 @@ __device__ __forceinline__ void walk_tile_lists(int tid, int cnt, LoadList&& loa
 // approximations (same acc, same c). Returns false, uniformly, when the
 // survivors overflow cap (e.g. fewer than k positive scores: tau = 0); acc
 // is untouched, so the caller then runs the all-songs path.
+#ifndef MR_CAND_EB
+#define MR_CAND_EB 4  // wide_cand_topk: songs per thread whose loads are issued together (5 / 7 slower, 10 spilled)
+#endif
+#ifndef MR_CAND_PRE
+#define MR_CAND_PRE 1  // the first batch's scales loaded by the caller before stage 2's last barrier
+#endif
 template <int MODEL, int NT, int EMAX>
 __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsigned long long* acc,
                                                const unsigned* heard, int blo, int bw, int k, unsigned char* gm,
                                                long long* ck, int* cs, int cap, long long* fk, int* fs,
-                                               long long* sb) {
+                                               long long* sb, bool have_rv, const float (&pre_rv)[MR_CAND_EB]) {
   constexpr int NG = NT / 16;
   const int tid = threadIdx.x;
   float ap[EMAX];
   long long mk = kKeyNone;
   int ms = INT_MAX;
-#ifndef MR_CAND_EB
-#define MR_CAND_EB 4
-#endif
-  constexpr int EB = MR_CAND_EB;  // songs per thread whose loads are issued together (10 spilled)
+  constexpr int EB = MR_CAND_EB;
 #pragma unroll
   for (int e0 = 0; e0 < EMAX; e0 += EB) {
     unsigned long long av[EB];
@@ -1813,7 +1819,7 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
         av[j] = acc[i];
         // (loading these at the kernel's start, in flight during stage 2, ran
         // 41.46 vs 41.08 ms at C4: profiles/r05/s2)
-        rv[j] = MODEL == MR_IBM ? p.rsq_c[blo + i] : 1.f;
+        rv[j] = MODEL != MR_IBM ? 1.f : (e0 == 0 && have_rv) ? pre_rv[j] : p.rsq_c[blo + i];
       }
     }
 #pragma unroll
@@ -1966,6 +1972,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
   __syncthreads();
   MR_STAMP(1);
 
+  bool have_rv = false;  // (COOC, p.cand: pass A's first scales loaded at the end of stage 2)
+  float pre_rv[MR_CAND_EB];
   if constexpr (COOC) {
     // stage 2 from the co-listening index: acc[s] += q(s2) * C[s2][s] over
     // u's index rows' segments in this tile. Dense segments (every song's
@@ -2035,12 +2043,66 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         constexpr int DS = kDenseDS;
         typedef unsigned dvec_t __attribute__((ext_vector_type(DS / 4)));
         // chunk c = b0 / DS: songs cooc_dense_song(c, i) (wave-uniform block)
+        constexpr int DU = MR_COOC_DU;  // dense rows per step, their loads issued together
+#if MR_COOC_SPLIT
+        if (p.frac_bits <= 32) {
+          // q <= 2^32: its 16-bit halves times the count bytes summed in u32
+          // (v_mad_u32_u24; <= 255 rows x 255 x 2^16 < 2^32), the row
+          // descriptors read from lanes (v_readlane: scalar, no LDS round trip
+          // before each row's load)
+          for (int b0 = DS * tid; (b0 & ~(kDenseBlock - 1)) < bw; b0 += DS * NT) {
+            unsigned lo[DS], hi[DS];
+#pragma unroll
+            for (int i = 0; i < DS; ++i) lo[i] = hi[i] = 0u;
+            for (int g0 = 0; g0 < nd; g0 += 64) {
+              const int dj = g0 + lane, ng = min(64, nd - g0);
+              const long long mo = dj < nd ? d_off[dj] : 0;
+              const unsigned long long mq = dj < nd ? d_q[dj] : 0ull;
+              const int mo_lo = (int)(unsigned)mo, mo_hi = (int)(mo >> 32), mq_lo = (int)(unsigned)mq,
+                        mq_hi = (int)(mq >> 32);
+              for (int d0 = 0; d0 < ng; d0 += DU) {
+                dvec_t v0[DU];
+                unsigned ql[DU], qh[DU];
+#pragma unroll
+                for (int j = 0; j < DU; ++j) {
+                  const int d = d0 + j;
+                  v0[j] = dvec_t(0u);
+                  ql[j] = qh[j] = 0u;
+                  if (d < ng) {
+                    const long long off = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(mo_hi, d)
+                                                       << 32) |
+                                                      (unsigned)__builtin_amdgcn_readlane(mo_lo, d));
+                    const unsigned long long q =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(mq_hi, d) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane(mq_lo, d);
+                    ql[j] = (unsigned)(q & 0xffffu);
+                    qh[j] = (unsigned)(q >> 16);
+                    v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + off + (b0 >> 2));
+                  }
+                }
+#pragma unroll
+                for (int j = 0; j < DU; ++j) {
+#pragma unroll
+                  for (int i = 0; i < DS; ++i) {
+                    const unsigned c = (v0[j][i >> 2] >> (8 * (i & 3))) & 0xffu;
+                    lo[i] += __umul24(c, ql[j]);
+                    hi[i] += __umul24(c, qh[j]);
+                  }
+                }
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < DS; ++i) {
+              const int col = cooc_dense_song(b0 / DS, i);
+              if (col < bw) acc[col] += ((unsigned long long)hi[i] << 16) + lo[i];
+            }
+          }
+        } else
+#endif
         for (int b0 = DS * tid; (b0 & ~(kDenseBlock - 1)) < bw; b0 += DS * NT) {
           unsigned long long aa[DS];
 #pragma unroll
           for (int i = 0; i < DS; ++i) aa[i] = 0ull;
-          // DU dense rows per step, their loads issued together
-          constexpr int DU = MR_COOC_DU;
           for (int d0 = 0; d0 < nd; d0 += DU) {
             dvec_t v0[DU];
             unsigned long long qd[DU];
@@ -2114,6 +2176,14 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
             if (wq[j][i])
               atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
       }
+      if (MR_CAND_PRE && p.cand && c0 + p.nseg >= t1) {  // the last pass: pass A's first scales
+#pragma unroll
+        for (int e = 0; e < MR_CAND_EB; ++e) {
+          const int i = tid + e * NT;
+          pre_rv[e] = i < bw ? p.rsq_c[blo + i] : 0.f;
+        }
+        have_rv = true;
+      }
       __syncthreads();  // the next pass rewrites the descriptors
       MR_STAMP(14);  // sparse segments walked
     }
@@ -2159,7 +2229,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 #endif
   if (p.cand) {
     have = wide_cand_topk<MODEL, NT, kCandE>(p, acc, heard, blo, bw, k, smem_raw + L.gm, wk, ws,
-                                             min(256, NW * k), fk, fs, sbp);
+                                             min(256, NW * k), fk, fs, sbp, have_rv, pre_rv);
     MR_STAMP(6);
   }
   if (!have) {
