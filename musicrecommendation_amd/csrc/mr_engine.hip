@@ -1624,6 +1624,10 @@ constexpr int kWideThreads = 1024;
 #ifndef MR_COOC_SPLIT
 #define MR_COOC_SPLIT 1     // co-listening scoring: the dense pass's u32 half-weight sums (frac_bits <= 32)
 #endif
+#ifndef MR_COOC_DOT2
+#define MR_COOC_DOT2 1      // co-listening scoring: the split dense pass two rows per v_dot2_u32_u16
+#endif
+typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
@@ -1803,8 +1807,10 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
   constexpr int NG = NT / 16;
   const int tid = threadIdx.x;
   float ap[EMAX];
-  long long mk = kKeyNone;
-  int ms = INT_MAX;
+  // the thread's best approximation and its slot: songs ascend with e, so a
+  // strictly larger value is the (key desc, song asc) order's better one
+  float ba = -1.f;
+  int be = -1;
   constexpr int EB = MR_CAND_EB;
 #pragma unroll
   for (int e0 = 0; e0 < EMAX; e0 += EB) {
@@ -1831,11 +1837,15 @@ __device__ __forceinline__ bool wide_cand_topk(const ScoreParams& p, const unsig
       if (i < bw && !((heard[i >> 5] >> (i & 31)) & 1u)) {
         const float hi = (float)(unsigned)(av[j] >> 32), lo = (float)(unsigned)av[j];
         a = __fmaf_rn(hi, 4294967296.f, lo) * rv[j];
-        take_if_before(mk, ms, (long long)__float_as_uint(a), blo + i);
       }
+      be = a > ba ? e : be;
+      ba = a > ba ? a : ba;
       ap[e] = a;
     }
   }
+  // (non-negative floats order as their bit patterns: the key of a)
+  const long long mk = be >= 0 ? (long long)__float_as_uint(ba) : kKeyNone;
+  const int ms = be >= 0 ? blo + tid + be * NT : INT_MAX;
   MR_STAMP(3);
   long long tk;
   int tsg;
@@ -2080,6 +2090,36 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
                     v0[j] = *reinterpret_cast<const dvec_t*>(p.pool + off + (b0 >> 2));
                   }
                 }
+#if MR_COOC_DOT2
+                // two rows per v_dot2_u32_u16: a song's two count bytes as a
+                // u16 pair (one v_perm_b32) times the rows' weight halves —
+                // 1.5 VALU per count byte; a row with q = 2^32 (q >> 16 =
+                // 2^16, one listener) takes the u24 path with its partner
+                static_assert(DU % 2 == 0, "row pairs");
+#pragma unroll
+                for (int j = 0; j < DU; j += 2) {
+                  if (qh[j] <= 0xffffu && qh[j + 1] <= 0xffffu) {
+                    const us2_t qlp = __builtin_bit_cast(us2_t, ql[j] | (ql[j + 1] << 16));
+                    const us2_t qhp = __builtin_bit_cast(us2_t, qh[j] | (qh[j + 1] << 16));
+#pragma unroll
+                    for (int i = 0; i < DS; ++i) {
+                      const unsigned sel = 0x0c000c00u | ((4u + (i & 3)) << 16) | (unsigned)(i & 3);
+                      const us2_t c2 = __builtin_bit_cast(us2_t, __builtin_amdgcn_perm(v0[j + 1][i >> 2], v0[j][i >> 2], sel));
+                      lo[i] = __builtin_amdgcn_udot2(c2, qlp, lo[i], false);
+                      hi[i] = __builtin_amdgcn_udot2(c2, qhp, hi[i], false);
+                    }
+                  } else {
+#pragma unroll
+                    for (int jj = j; jj < j + 2; ++jj)
+#pragma unroll
+                      for (int i = 0; i < DS; ++i) {
+                        const unsigned c = (v0[jj][i >> 2] >> (8 * (i & 3))) & 0xffu;
+                        lo[i] += __umul24(c, ql[jj]);
+                        hi[i] += __umul24(c, qh[jj]);
+                      }
+                  }
+                }
+#else
 #pragma unroll
                 for (int j = 0; j < DU; ++j) {
 #pragma unroll
@@ -2089,6 +2129,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
                     hi[i] += __umul24(c, qh[j]);
                   }
                 }
+#endif
               }
             }
 #pragma unroll
