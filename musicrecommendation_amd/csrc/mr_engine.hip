@@ -2182,6 +2182,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       int cur = -1, ce = 0;
       long long co = 0;
       unsigned long long cq = 0ull;
+      const unsigned pad_x = (unsigned)lane << kCoocCntBits;
       for (int e0 = 4 * tid; e0 < total; e0 += 4 * U * NT) {
         unsigned x[U][4];
         unsigned long long wq[U][4];
@@ -2189,7 +2190,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
         for (int j = 0; j < U; ++j) {
           const int e = e0 + j * 4 * NT;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { x[j][i] = 0u; wq[j][i] = 0ull; }
+          for (int i = 0; i < 4; ++i) { x[j][i] = pad_x; wq[j][i] = 0ull; }
           if (e < total) {
             while (e >= ce) { ++cur; ce = m_pre[cur + 1]; co = m_off[cur]; cq = m_q[cur]; }
             if (e + 3 < ce) {
@@ -2210,12 +2211,13 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
             }
           }
         }
+        // (no branch per entry: a slot past the list adds 0 at song lane < 64,
+        // distinct per lane — inside acc, never read past bw)
 #pragma unroll
         for (int j = 0; j < U; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (wq[j][i])
-              atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
+            atomicAdd(&acc[x[j][i] >> kCoocCntBits], (unsigned long long)(x[j][i] & kCoocCntMask) * wq[j][i]);
       }
       if (MR_CAND_PRE && p.cand && c0 + p.nseg >= t1) {  // the last pass: pass A's first scales
 #pragma unroll
