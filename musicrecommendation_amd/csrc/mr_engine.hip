@@ -3214,16 +3214,28 @@ __device__ __forceinline__ int group_chunk(const unsigned* songs, unsigned x, un
   return m >= 4u ? 4 : (int)m;
 }
 
-// A chunk's m valid songs counted (u16 pairs: song x's counter is the half
-// x & 1 of word x >> 1; fire-and-forget LDS adds).
+// Song key's counter + 1 (u16 pairs: song x's counter is the half x & 1 of
+// word x >> 1; a fire-and-forget LDS add). MR_GROUP_PAD: no branch per key —
+// an invalid slot adds 0 to the lane's own word (< 64, inside the counters).
+#ifndef MR_GROUP_PAD
+#define MR_GROUP_PAD 1
+#endif
+__device__ __forceinline__ void group_inc(unsigned* cnt, unsigned key, bool ok, unsigned lo0) {
+#if MR_GROUP_PAD
+  const unsigned x = ok ? key - lo0 : 2u * (threadIdx.x & 63u);
+  atomicAdd(&cnt[x >> 1], ok ? 1u << ((x & 1u) << 4) : 0u);
+#else
+  if (ok) {
+    const unsigned x = key - lo0;
+    atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
+  }
+#endif
+}
+// A chunk's m valid songs counted.
 __device__ __forceinline__ void group_add(unsigned* cnt, const u32x4_a4& c, int m, unsigned lo0) {
   const unsigned k[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (i < m) {
-      const unsigned x = k[i] - lo0;
-      atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
-    }
+  for (int i = 0; i < 4; ++i) group_inc(cnt, k[i], i < m, lo0);
 }
 
 // k_cooc_group's rows under kCoocBigRow listeners, every tile group in turn
@@ -3387,11 +3399,7 @@ __global__ __launch_bounds__(NT) void k_cooc_group(CoocParams p) {
     rows_walk(tid, NT, glog, [](int l) { return l; }, n, GroupRange{lst, p.lrec_words, gi}, p.sr_songs,
               [&](const unsigned (&k)[8], int m) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
-                  if (i < m) {
-                    const unsigned x = k[i] - (unsigned)lo0;
-                    atomicAdd(&cnt[x >> 1], 1u << ((x & 1u) << 4));
-                  }
+                for (int i = 0; i < 8; ++i) group_inc(cnt, k[i], i < m, (unsigned)lo0);
               });
     __syncthreads();
     if (gi == g_begin) stamp_rt(sb, 1);  // the first group's walk done
