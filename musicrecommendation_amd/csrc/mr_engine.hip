@@ -1628,6 +1628,9 @@ constexpr int kWideThreads = 1024;
 #define MR_COOC_DOT2 1      // co-listening scoring: the split dense pass two rows per v_dot2_u32_u16
 #endif
 typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
+#ifndef MR_COOC_NOZERO
+#define MR_COOC_NOZERO 1    // co-listening scoring: acc zeroed only when the first pass has no dense row
+#endif
 #ifndef MR_GROUP_STUB
 #define MR_GROUP_STUB 0     // timing-only builds of k_cooc_group's emission (1: no sparse stores, 2: pass A only)
 #endif
@@ -1948,11 +1951,18 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       pf_s = p.te_songs[a + tid];
     }
   }
+  // co-listening route (MR_COOC_NOZERO): a first descriptor pass with dense
+  // rows STORES every song's dense sum (the pass covers the whole tile), so
+  // acc is zeroed here only for users without index rows, else after the
+  // first pass's scan when it has no dense row
+  auto zero_acc = [&]() {
 #if MR_WIDE_Z16  // 16-B stores: two songs per store (acc is 16-B aligned; bs is even)
-  for (int i = tid; 2 * i < bw; i += NT) reinterpret_cast<ulonglong2*>(acc)[i] = make_ulonglong2(0ull, 0ull);
+    for (int i = tid; 2 * i < bw; i += NT) reinterpret_cast<ulonglong2*>(acc)[i] = make_ulonglong2(0ull, 0ull);
 #else
-  for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
+    for (int i = tid; i < bw; i += NT) acc[i] = 0ull;
 #endif
+  };
+  if (!(COOC && MR_COOC_NOZERO) || p.te_off[u + 1] == p.te_off[u]) zero_acc();
   if constexpr (kDPF) {
     if (pf_r >= 0) {
       pf_sl = p.seg_len[(size_t)tile * p.n_rows + pf_r];
@@ -2046,6 +2056,11 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       if (tid == 0) m_pre[ns] = total;
       __syncthreads();
       MR_STAMP(12);  // (the last descriptor pass's) descriptors ready
+      const bool store = MR_COOC_NOZERO && c0 == t0;  // the first pass: dense sums stored, else zeroed here
+      if (store && nd == 0) {
+        zero_acc();
+        __syncthreads();
+      }
       if (nd > 0) {
         // DS songs per thread per block of DS * NT, every dense row summed in
         // registers (DS = 8: one 8-B load per row; 16: one 16-B load per row,
@@ -2135,7 +2150,8 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 #pragma unroll
             for (int i = 0; i < DS; ++i) {
               const int col = cooc_dense_song(b0 / DS, i);
-              if (col < bw) acc[col] += ((unsigned long long)hi[i] << 16) + lo[i];
+              const unsigned long long v = ((unsigned long long)hi[i] << 16) + lo[i];
+              if (col < bw) acc[col] = store ? v : acc[col] + v;
             }
           }
         } else
@@ -2169,7 +2185,7 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
 #pragma unroll
           for (int i = 0; i < DS; ++i) {
             const int col = cooc_dense_song(b0 / DS, i);
-            if (col < bw) acc[col] += aa[i];
+            if (col < bw) acc[col] = store ? aa[i] : acc[col] + aa[i];
           }
         }
         __syncthreads();  // the sparse walk's atomics may hit any song
