@@ -608,6 +608,19 @@ __device__ __forceinline__ void topk_dst_write(const TopkDst& d, int slot, long 
   if (d.score) d.score[slot] = key >= 0 ? __longlong_as_double(key) : (double)NAN;
 }
 
+// key / bs for shard-local songs (< 2^24) without an integer division: the
+// fp32 quotient is within one of the truth, then corrected
+#ifndef MR_LIGHT_FDIV
+#define MR_LIGHT_FDIV 1
+#endif
+__device__ __forceinline__ int tile_of(int key, int bs, float inv_bs) {
+  if (!MR_LIGHT_FDIV) return key / bs;
+  int t = (int)((float)key * inv_bs);
+  t -= t * bs > key ? 1 : 0;
+  t += (t + 1) * bs <= key ? 1 : 0;
+  return t;
+}
+
 // Ranks of nc <= 256 survivor candidates ck/cs among themselves (total order
 // (key desc, song asc)): rank < k -> output slot; slots past nc get (-1, -1).
 // crank: 256 zeroed ints. All threads call it; it ends with a barrier (not
@@ -2947,9 +2960,10 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
   stamp_rt(sb, 2);
   // emit: per-tile counts, segment offsets, then the entries
   const int bs = p.block_songs;
+  const float inv_bs = 1.0f / (float)bs;
   for (int i = tid; i < S; i += NT) {
     const unsigned x = tab[i];
-    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
+    if (x) atomicAdd(&tcnt[tile_of((int)((x >> kLightCntBits) - 1u), bs, inv_bs)], 1);
   }
   __syncthreads();
   stamp_rt(sb, 3);
@@ -2978,7 +2992,7 @@ __global__ __launch_bounds__(NT) void k_cooc_light(CoocParams p) {
     const unsigned x = tab[i];
     if (x) {
       const int key = (int)((x >> kLightCntBits) - 1u);
-      const int t = key / bs;
+      const int t = tile_of(key, bs, inv_bs);
       const int pos = atomicAdd(&tpos[t], 1);
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
@@ -3024,9 +3038,10 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
   wave_lds_sync();
   stamp_rt_wave(sb, 2);
   const int bs = p.block_songs;
+  const float inv_bs = 1.0f / (float)bs;
   for (int i = lane; i < S; i += 64) {
     const unsigned x = tab[i];
-    if (x) atomicAdd(&tcnt[(int)((x >> kLightCntBits) - 1u) / bs], 1);
+    if (x) atomicAdd(&tcnt[tile_of((int)((x >> kLightCntBits) - 1u), bs, inv_bs)], 1);
   }
   wave_lds_sync();
   {
@@ -3050,7 +3065,7 @@ __global__ __launch_bounds__(64 * kWaveRowsPerBlock) void k_cooc_light_wave(Cooc
     const unsigned x = tab[i];
     if (x) {
       const int key = (int)((x >> kLightCntBits) - 1u);
-      const int t = key / bs;
+      const int t = tile_of(key, bs, inv_bs);
       const int pos = atomicAdd(&tpos[t], 1);
       out[pos] = ((unsigned)(key - t * bs) << kCoocCntBits) | (x & kLightCntMask);
     }
