@@ -610,6 +610,9 @@ __device__ __forceinline__ void topk_dst_write(const TopkDst& d, int slot, long 
 
 // key / bs for shard-local songs (< 2^24) without an integer division: the
 // fp32 quotient is within one of the truth, then corrected
+#ifndef MR_LIGHT_CAS1
+#define MR_LIGHT_CAS1 1
+#endif
 #ifndef MR_LIGHT_FDIV
 #define MR_LIGHT_FDIV 1
 #endif
@@ -2893,12 +2896,19 @@ __device__ __forceinline__ void light_insert_queue(unsigned* tab, unsigned mask,
   unsigned h = (q[0] * 2654435761u) >> sh;
   int left = m;
   while (left > 0) {
+#if MR_LIGHT_CAS1
+    // the CAS first: a new key (most keys: counts of light rows are mostly 1)
+    // takes one LDS round trip instead of a read and then the CAS
+    unsigned x = atomicCAS(&tab[h], 0u, tag | 1u);
+    bool done = x == 0u;
+#else
     unsigned x = tab[h];
     bool done = false;
     if (x == 0u) {
       x = atomicCAS(&tab[h], 0u, tag | 1u);
       done = x == 0u;
     }
+#endif
     if (!done && (x & ~kLightCntMask) == tag) {
       atomicAdd(&tab[h], 1u);
       done = true;
