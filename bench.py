@@ -252,47 +252,55 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     """Config 5: the reference's whole evaluation pipeline on device — ubm + ibm
     dense models, linear / aggregation / stochastic combinations (main.scala:57-89,
     MR:317-481) and the threshold mAP of all five (MR:636), 2,000 test users
-    against the full train set. N > 1: the 2-D layout of sharding.ShardScorer
-    (--shard songs: song shards only; users: test-user blocks only); combinations
-    are per pair, the mAP reductions (MIN/MAX, count SUM) go over RCCL."""
+    against the full train set. N > 1 (--c5-layout models, the default):
+    sharding.EnsembleScorer — ubm by test-user blocks, ibm by song shards, ONE
+    all-to-all of the ibm rows into the blocks, the combinations and the five
+    mAPs on the blocks (one MAX + one SUM all-reduce over RCCL); --c5-layout
+    grid: both models in the 2-D layout of sharding.ShardScorer (--shard)."""
     from musicrecommendation_amd import evaluation
     from musicrecommendation_amd.ensemble import DeviceEnsemble
-    from musicrecommendation_amd.sharding import layout_2d, shard_tile, song_shards, user_blocks
+    from musicrecommendation_amd.sharding import EnsembleScorer, layout_2d, shard_tile, song_shards, user_blocks
 
     n_tr, n_te, _seed = synth.BULK_CONFIGS["c5"]
-    trip = synth.config("c5")
-    full = trip.dataset()
-    gs, gu = layout_2d(world, song_groups_for(args, world))
-    a, b = user_blocks(full.n_test, gu)[rank // gs]
-    lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu, n_songs=full.n_songs,
-                                              n_shards=gs))[rank % gs]
-    ds = full if gu == 1 else full.subset_test_users(a, b)
-    eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi, ibm_route=args.ibm_route)
-    ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),
-                         pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs,
-                         collectives=True if _pg() else None)
-    maps = {}
+    full, setup_s = shared_bulk_dataset("c5", world, rank)  # N > 1: rank 0 generates, the others load
+    coll = True if _pg() else None
+    if args.c5_layout == "models":
+        sc = EnsembleScorer(full, rank, world, local, out_dtype="f32", ibm_route=args.ibm_route, collectives=coll)
+        ens, eng, ds = sc.ens, sc.eng_i, full
+        layout = f"ubm: users{world} blocks, ibm: songs{world} shards, one all-to-all" if world > 1 else "songs1xusers1"
 
-    def step():
-        ubm, ibm = ens.model("ubm"), ens.model("ibm")
-        # the three combinations in one pass, their min / max carried to threshold_map
-        lcm, am, scm = ens.combinations(ubm, ibm, 0.5, 0.5, 0.5, seed=1)
-        models = {"ubm": ubm, "ibm": ibm, "lcm": lcm, "am": am, "scm": scm}
-        for name, t in models.items():
-            maps[name] = ens.threshold_map(t)
-        return models
+        def step():
+            return sc.step(0.5, 0.5, 0.5, seed=1)
+    else:
+        sc = None
+        gs, gu = layout_2d(world, song_groups_for(args, world))
+        a, b = user_blocks(full.n_test, gu)[rank // gs]
+        lo, hi = song_shards(full, gs, shard_tile(full.n_train, full.n_test // gu, n_songs=full.n_songs,
+                                                  n_shards=gs))[rank % gs]
+        ds = full if gu == 1 else full.subset_test_users(a, b)
+        eng = Engine(ds, device=local, out_dtype="f32", topk=10, song_lo=lo, song_hi=hi, ibm_route=args.ibm_route)
+        ens = DeviceEnsemble(eng, pair_base=a * full.n_songs - int(full.te_off[a]), n_pairs=full.n_pairs(),
+                             pos=evaluation.label_pos(full), n_label_songs=full.n_label_songs, collectives=coll)
+        layout = f"songs{gs}xusers{gu}"
+
+        def step():
+            ubm, ibm = ens.model("ubm"), ens.model("ibm")
+            # the three combinations in one pass, their min / max carried to threshold_map
+            lcm, am, scm = ens.combinations(ubm, ibm, 0.5, 0.5, 0.5, seed=1)
+            models = {"ubm": ubm, "ibm": ibm, "lcm": lcm, "am": am, "scm": scm}
+            return models, ens.threshold_maps(models)
 
     models = None
     for _ in range(args.warmup):
         models = None  # release the previous step's buffers so the allocator reuses them
-        models = step()
+        models, maps = step()
     if _pg():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         models = None
-        models = step()
+        models, maps = step()
     torch.cuda.synchronize()
     if _pg():
         dist.barrier()
@@ -301,15 +309,19 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
     if _pg():
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
+    songs = None
+    if world == 1:
+        songs, _sc, _k = ens.topk(models["lcm"])
     if rank == 0:
         pairs = full.n_pairs()
         value = pairs * args.steps / elapsed
-        songs, _sc, _k = ens.topk(models["lcm"])  # this rank's cell when world > 1
         ab = algorithmic_bytes(full, 4, 10)
         model_bytes = sum(ab.values())
         ibm_bytes = model_bytes
         if eng.ibm_route == "cooc":  # the ibm model's byte model on its route (counts of the last ibm run)
-            ibm_bytes = sum(cooc_bytes(eng, ds, 4, 10).values())
+            ibm_bytes = sum(cooc_bytes(eng, eng.dataset, 4, 10).values())
+            if world > 1:  # rank 0's song shard: the whole model's ~ N x that (shards cut equal)
+                ibm_bytes *= world
         dense_elems = full.n_test * full.n_songs
         # per step: 2 models + the combinations' one pass (2 reads + 3 writes) + min/max reads of the
         # 2 models (the combinations carry theirs) + 5 counts reads
@@ -331,10 +343,12 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
             "config": {"workload": f"c5: {n_tr} train / {n_te} test / {full.n_songs} songs; ubm + ibm dense fp32, "
                                    f"linear(0.5) + aggregation(0.5) + stochastic(0.5, seed 1), threshold mAP x5",
                        "n_train": n_tr, "n_test": n_te, "n_songs": full.n_songs, "pairs_per_step": pairs,
-                       "parallelism": f"songs{gs}xusers{gu}"},
+                       "parallelism": layout},
+            "exchange_bytes_per_rank": sc.exchange_bytes if sc is not None and world > 1 else None,
+            "setup_dataset_s": setup_s,
             "roofline": {"bound": "hbm", "kernel": "whole step (2 scoring passes + 3 combinations + 5 evaluations)",
-                         "achieved": step_bytes / step_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS, "traffic": traffic,
+                         "achieved": step_bytes / step_s / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                         "frac": step_bytes / step_s / 1e9 / (HBM_PEAK_GBS * world), "traffic": traffic,
                          "traffic_source": "profiles/pmc_c5.json (rocprofv3 --pmc passes over one step, every "
                                            "engine kernel summed)" if traffic else None,
                          "traffic_GBps": traffic / step_s / 1e9 if traffic else None,
@@ -343,16 +357,67 @@ def run_c5(args, world: int, rank: int, local: int) -> None:
                          "traffic_frac": traffic / step_s / 1e9 / HBM_PEAK_GBS if traffic else None,
                          "algorithmic_bytes_per_step": step_bytes},
             "threshold_mAP": maps,
-            "mAP@10_lcm": evaluation.map_at_k(songs, full, 10) if world == 1 else None,
+            "mAP@10_lcm": evaluation.map_at_k(songs, full, 10) if songs is not None else None,
             "cpu_baseline": (cpu_baseline_twohop(full, "ibm", args.cpu_baseline_seconds)
                              if world == 1 and not args.no_cpu_baseline else None),
         }
         if world == 1 and not args.no_e2e:
-            line["end_to_end"] = end_to_end_bulk(trip, "ibm")
+            models = None
+            if sc is not None:
+                sc.close()
+                sc = None
+            line["end_to_end"] = end_to_end_c5(synth.config("c5"))
         print(json.dumps(line), flush=True)
-    eng.close()
+    if sc is not None:
+        sc.close()
+    else:
+        eng.close()
     if _pg():
         dist.destroy_process_group()
+
+
+def end_to_end_c5(trip, reps: int = 2):
+    """C5's own pipeline on one GPU, wall clock: ingest of the three TSV files
+    (native reader, ≙ the MusicRecommender constructor, MR:26-91) -> mr_load
+    (host index build + H2D) -> both dense models, the three combinations and
+    the five threshold mAPs (main.scala:37-89 without the prints: the mAP
+    values are the pipeline's output, MR:636). Median of `reps` runs; the files
+    are written once beforehand (untimed)."""
+    import tempfile
+
+    from musicrecommendation_amd.dataset import Dataset
+    from musicrecommendation_amd.sharding import EnsembleScorer
+
+    rows = []
+    with tempfile.TemporaryDirectory() as td:
+        paths = [os.path.join(td, n) for n in ("train.txt", "test.txt", "labels.txt")]
+        t0 = time.perf_counter()
+        nbytes = trip.write_tsv(*paths)
+        write_s = time.perf_counter() - t0
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            d2 = Dataset.from_tsv(*paths)
+            t1 = time.perf_counter()
+            sc = EnsembleScorer(d2, 0, 1, torch.cuda.current_device(), out_dtype="f32")
+            t2 = time.perf_counter()
+            models, maps = sc.step(0.5, 0.5, 0.5, seed=1)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            del models
+            sc.close()
+            rows.append((t3 - t0, t1 - t0, t2 - t1, t3 - t2))
+            del d2
+    rows.sort()
+    tot, ing, load, run = rows[len(rows) // 2]
+    n_rows = int(trip.train_u.size + trip.test_u.size + trip.label_u.size)
+    return {"ms": tot * 1e3, "rows": n_rows, "tsv_bytes": nbytes,
+            "breakdown_ms": {"ingest_tsv": ing * 1e3, "mr_load_index_h2d": load * 1e3,
+                             "models_combinations_5_maps": run * 1e3},
+            "ingest_rows_per_s": n_rows / ing, "host_cores": host_cores()["threads"],
+            "note": f"wall clock, one GPU, median of {reps}: native TSV ingest (mr_corpus_from_tsv) + mr_load + "
+                    f"ubm + ibm dense models + the three combinations + the five threshold mAPs (the values the "
+                    f"reference's driver prints); files written beforehand in {write_s:.1f} s (untimed)"}
 
 
 def song_groups_for(args, world: int) -> int:
@@ -654,6 +719,9 @@ def main() -> None:
                     help="N > 1 layout: test-user blocks (default), song-range shards + all-gather of the "
                          "top-k lists (north star), or the 2-D product of both (--song-groups)")
     ap.add_argument("--song-groups", type=int, default=0, help="2d: song shards per user block")
+    ap.add_argument("--c5-layout", default="models", choices=["models", "grid"],
+                    help="C5 at N > 1: each model in its own layout (ubm by user blocks, ibm by song shards, "
+                         "one all-to-all; default) or both in the --shard grid")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (ingest + H2D + D2H) timing")
     ap.add_argument("--no-north-star", action="store_true",
                     help="skip the nested C4 2-D layout block (north_star) of the C2 line")

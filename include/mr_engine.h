@@ -174,8 +174,11 @@ int mr_route_info(const mr_ctx* ctx, int32_t* route, int32_t* n_rows, int64_t* p
  * song first and compute the exact fp64 score (the oracle's operations) of the
  * candidates within a relative margin of the threshold only — lists, keys and
  * scores bit-identical to the all-songs path; 0 when every song's exact score
- * is computed (dense output, the fused / separate shapes, k > 64, or
- * MR_WIDE_CAND=0 in the environment at mr_load). */
+ * is computed. Candidate mode is on (mr_load's cand_on) only for the wide shape
+ * with all of: no dense output (so no dense min / max either), no per-tile
+ * lists (topk_lists = 0), 1 <= k <= 16 (the wide shape's own bound; the
+ * selection's k <= scoring threads / 16 holds for either kernel width), a song tile of at most 20 x scoring threads, and
+ * MR_WIDE_CAND unset or not "0" in the environment at mr_load. */
 int mr_topk_mode(const mr_ctx* ctx, int32_t* candidate_only);
 
 /* Sizes of the latest ibm run on the co-listening route (the byte model of
@@ -391,6 +394,24 @@ int mr_eval_map(int32_t n_classes, const int32_t* pred_counts, const int32_t* tp
 int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
                        const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out,
                        int32_t n_thresholds);
+/* The multi-rank evaluation without the counts crossing PCIe (MR:541-627 over
+ * a model spread across ranks — song shards, test-user blocks or both):
+ * mr_eval_class_counts_device writes the counts of the label classes only into
+ * a caller DEVICE buffer laid out by a class list every rank shares —
+ * counts[0][c][t] = pred, counts[1][c][t] = tp of class c (2 x n_classes x
+ * n_thresholds int32), 0 for classes outside the context's song range — so one
+ * SUM all-reduce of the buffers over the ranks (RCCL) gives the counts over
+ * every test user; classes: host, strictly ascending global song ids
+ * (< n_songs; the songs with label count pos > 0: label-only songs are never
+ * predicted and add 0 to the sum). mr_eval_map_counts_device then computes the
+ * AP per class on the device from such a (reduced) buffer (class_pos: host,
+ * each > 0) and the mean over n_label_songs, classes summed in song-id order —
+ * bit-equal to mr_eval_map over the full counts. Both synchronous. */
+int mr_eval_class_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                                const int32_t* lab_songs, int32_t n_classes, const int32_t* classes,
+                                int32_t* counts, int32_t n_thresholds);
+int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_classes, const int32_t* class_pos, const int32_t* counts,
+                              int32_t n_label_songs, double* map_out, int32_t n_thresholds);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
  * (0 = separate stage-1 kernel — neighbour lists —, 1 = the

@@ -4581,6 +4581,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
         const int bw = (int)(std::min<int64_t>(width, (int64_t)(t + 1) * bs) - (int64_t)t * bs);
         dense_pad += cooc_dense_words(bw) - (bw + 3) / 4;
       }
+      // whole 16-B words: every row's bound stays a multiple of 4 words, so
+      // every row (placed by the exclusive scan below) starts 16-B aligned for
+      // the scorer's dvec_t loads and k_cooc_group's chunk_t stores
+      dense_pad = (dense_pad + 3) & ~(int64_t)3;
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
         if (light_ok && row_base[r] * 100 <= light_slots_max * lload && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
@@ -4661,9 +4665,29 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       }
       pool_cap = mr_par::exclusive_scan(row_base.data(), nr);
       row_base[nr] = pool_cap;
+      for (int64_t r = 0; r < nr; ++r)
+        if (row_base[r] & 3)
+          return fail(MR_E_STATE, "co-listening index: row %lld starts at word %lld (not 16-B aligned)",
+                      (long long)r, (long long)row_base[r]);
+      // the pool and the per-(row, listener) record tables built beside it:
+      // lrec (the u16 heavy rows' listeners, lrec_words each), llrec (8 B per
+      // light-row listener) and urec (alive during the load), against half the
+      // free device memory (the share of it a group's context may use)
+      double rec_b = 0.0;
+      {
+        int64_t n_lrec = 0, n_llrec = 0;
+        for (size_t i = 0; i < heavy_rows.size(); ++i)
+          if (grp > 0 && (int)i >= n_heavy32) n_lrec += col_tr[row_song[heavy_rows[i]]];
+        for (int32_t r : light_rows) n_llrec += col_tr[row_song[r]];
+        int lw = 1;
+        const int ng = grp > 0 ? (n_tiles + grp - 1) / grp : 0;
+        while (2 * (lw - 1) < ng + 1) lw <<= 1;
+        rec_b = 4.0 * (double)n_lrec * lw + 8.0 * (double)n_llrec + 4.0 * (double)n_tr * urec_words;
+      }
       size_t free_b = 0, total_b = 0;
       MR_HIP(hipMemGetInfo(&free_b, &total_b));
-      if ((double)pool_cap * 4.0 > 0.5 * (double)free_b) why = "a pool within half the free device memory";
+      if ((double)pool_cap * 4.0 + rec_b > 0.5 * (double)free_b / std::max(1, c->dev_share))
+        why = "a pool within half the free device memory";
     }
     if (c->opt.ibm_route == 2 && why)
       return fail(MR_E_INVALID, "ibm_route 2 (co-listening index) needs %s", why);

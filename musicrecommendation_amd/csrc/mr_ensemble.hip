@@ -399,6 +399,28 @@ __global__ __launch_bounds__(kThreads) void k_eval_ap(int n, int n_thr, const in
   ap[c] = a;
 }
 
+// The label classes' rows of the shard's counts, in a class-indexed block
+// that every rank lays out alike (the global class list): out[0][c][t] =
+// pred, out[1][c][t] = tp of class c when its song is in [song_lo, song_hi),
+// else 0 — so summing the blocks over ranks (one all-reduce) gives the counts
+// of MR:541-553 over every test user, whatever the layout.
+__global__ __launch_bounds__(kThreads) void k_eval_gather(int n_cls, int n_thr, int song_lo, int width,
+                                                          const int* cls, const int* pred, const int* tp,
+                                                          int* out) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= n_cls * n_thr) return;
+  const int c = j / n_thr, t = j - c * n_thr;
+  const int g = cls[c] - song_lo;
+  const bool in = g >= 0 && g < width;
+  out[j] = in ? pred[(size_t)g * n_thr + t] : 0;
+  out[(size_t)n_cls * n_thr + j] = in ? tp[(size_t)g * n_thr + t] : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_iota(int n, int* out) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j < n) out[j] = j;
+}
+
 template <typename T>
 struct Tmp {  // scratch device buffer of one call, stream-ordered (pool allocator: no device sync)
   T* p = nullptr;
@@ -648,6 +670,71 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
   MR_HIP(hipStreamSynchronize(st));
   double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
   for (int c = 0; c < nc; ++c) total += ap[c];
+  *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
+  return MR_OK;
+}
+
+int mr_eval_class_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
+                                const int32_t* lab_songs, int32_t n_classes, const int32_t* classes,
+                                int32_t* counts, int32_t n_thresholds) {
+  if (!counts || (n_classes > 0 && !classes) || n_classes < 0) return fail(MR_E_INVALID, "null argument");
+  for (int32_t c = 1; c < n_classes; ++c)
+    if (classes[c] <= classes[c - 1]) return fail(MR_E_INVALID, "classes not strictly ascending at %d", (int)c);
+  const int n_thr = thresholds_or_default(n_thresholds);
+  mr_view v;
+  Tmp<int> d_pred, d_tp;
+  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)v.stream;
+  if (n_classes > 0) {
+    Tmp<int> d_cls;
+    d_cls.st = st;
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)n_classes * 4, st));
+    MR_HIP(hipMemcpyAsync(d_cls.p, classes, (size_t)n_classes * 4, hipMemcpyHostToDevice, st));
+    const int n = n_classes * n_thr;
+    hipLaunchKernelGGL(k_eval_gather, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st, n_classes, n_thr,
+                       v.song_lo, v.song_hi - v.song_lo, d_cls.p, d_pred.p, d_tp.p, counts);
+    MR_HIP(hipGetLastError());
+    MR_HIP(hipStreamSynchronize(st));  // the host classes' staging copy has been read
+  }
+  MR_HIP(hipStreamSynchronize(st));
+  return MR_OK;
+}
+
+int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_classes, const int32_t* class_pos, const int32_t* counts,
+                              int32_t n_label_songs, double* map_out, int32_t n_thresholds) {
+  if (!ctx || !map_out || n_classes < 0 || (n_classes > 0 && (!class_pos || !counts)))
+    return fail(MR_E_INVALID, "null argument");
+  for (int32_t c = 0; c < n_classes; ++c)
+    if (class_pos[c] <= 0) return fail(MR_E_INVALID, "class %d has no positive (pos %d)", (int)c, (int)class_pos[c]);
+  const int n_thr = thresholds_or_default(n_thresholds);
+  if (n_thr != 10 && n_thr != 11)
+    return fail(MR_E_INVALID, "%d thresholds: 10 (MR:590) or 11 (distributed.scala:395)", n_thr);
+  mr_view v;
+  int rc = mr_view_get(ctx, &v);
+  if (rc) return rc;
+  MR_HIP(hipSetDevice(v.device));
+  hipStream_t st = (hipStream_t)v.stream;
+  std::vector<double> ap((size_t)std::max(1, n_classes));
+  if (n_classes > 0) {
+    Tmp<int> d_cls, d_cpos;
+    Tmp<double> d_ap;
+    d_cls.st = d_cpos.st = d_ap.st = st;
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)n_classes * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cpos.p), (size_t)n_classes * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)n_classes * 8, st));
+    MR_HIP(hipMemcpyAsync(d_cpos.p, class_pos, (size_t)n_classes * 4, hipMemcpyHostToDevice, st));
+    const int nb = (n_classes + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kThreads), 0, st, n_classes, d_cls.p);
+    // the class-indexed block: pred at [0][c][t], tp at [1][c][t]
+    hipLaunchKernelGGL(k_eval_ap, dim3(nb), dim3(kThreads), 0, st, n_classes, n_thr, d_cls.p, d_cpos.p, counts,
+                       counts + (size_t)n_classes * n_thr, d_ap.p);
+    MR_HIP(hipGetLastError());
+    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)n_classes * 8, hipMemcpyDeviceToHost, st));
+  }
+  MR_HIP(hipStreamSynchronize(st));
+  double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
+  for (int c = 0; c < n_classes; ++c) total += ap[c];
   *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
   return MR_OK;
 }

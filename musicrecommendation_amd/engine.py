@@ -287,6 +287,30 @@ class Engine:
             ctypes.byref(out), int(n_thresholds)), "mr_eval_map_device")
         return out.value
 
+    def eval_class_counts(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray, lab_songs: np.ndarray,
+                          classes: np.ndarray, counts_ptr: int, n_thresholds: int = 10) -> None:
+        """The label classes' (pred, tp) counts into a device buffer of
+        2 x len(classes) x n_thresholds int32 (mr_eval_class_counts_device;
+        classes: ascending global song ids, shared by every rank; 0 for classes
+        outside this context's songs), ready for a SUM all-reduce."""
+        lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
+        lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
+        classes = np.ascontiguousarray(classes, dtype=np.int32)
+        _lib.check(self._L.mr_eval_class_counts_device(
+            self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
+            lab_songs.ctypes.data_as(ctypes.c_void_p), int(classes.shape[0]), classes.ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_void_p(counts_ptr), int(n_thresholds)), "mr_eval_class_counts_device")
+
+    def eval_map_counts(self, counts_ptr: int, class_pos: np.ndarray, n_label_songs: int,
+                        n_thresholds: int = 10) -> float:
+        """mAP from a (reduced) class-count device buffer (mr_eval_map_counts_device)."""
+        class_pos = np.ascontiguousarray(class_pos, dtype=np.int32)
+        out = ctypes.c_double()
+        _lib.check(self._L.mr_eval_map_counts_device(
+            self._h, int(class_pos.shape[0]), class_pos.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(counts_ptr),
+            int(n_label_songs), ctypes.byref(out), int(n_thresholds)), "mr_eval_map_counts_device")
+        return out.value
+
     def timing_begin(self) -> None:
         """Open a timing window (one event on the engine stream)."""
         _lib.check(self._L.mr_timing_begin(self._h), "mr_timing_begin")

@@ -69,7 +69,8 @@ class DeviceEnsemble:
 
         self.e = engine
         self.ds = engine.dataset
-        self.device = torch.device("cuda", engine.opt.device)
+        # (host stand-ins of the CPU tests: torch's CPU device)
+        self.device = torch.device("cuda", engine.opt.device) if torch.cuda.is_available() else torch.device("cpu")
         self.torch_dtype = torch.float64 if engine.dtype == np.float64 else torch.float32
         self.shape = (engine.n_test, engine.width)
         self.pair_base = int(pair_base)
@@ -224,6 +225,59 @@ class DeviceEnsemble:
             c = c.cpu().numpy()
             full_p, full_t = c[0], c[1]
         return eval_map(full_p, full_t, self.pos, self.n_label_songs)
+
+    def _classes(self) -> Tuple[np.ndarray, np.ndarray]:
+        """The label classes every rank shares: ascending song ids with a label
+        (pos > 0; label-only songs are never predicted) and their label counts."""
+        if getattr(self, "_cls", None) is None:
+            cls = np.nonzero(self.pos > 0)[0].astype(np.int32)
+            self._cls = (cls, self.pos[cls].astype(np.int32))
+        return self._cls
+
+    def threshold_maps(self, models: dict, n_thresholds: int = 10) -> dict:
+        """evaluateModel (MR:636) of several dense device models, {name: mAP}.
+        One rank: threshold_map each (counts and AP on the device). Several
+        ranks (song shards, test-user blocks or both): ONE MAX all-reduce of
+        every model's (-min, max); the label classes' counts of every model into
+        one device block (mr_eval_class_counts_device, laid out by the global
+        class list, so any layout sums alike); ONE SUM all-reduce of that block
+        (RCCL; on a gloo group through the host); the AP per class on the device
+        (mr_eval_map_counts_device). Only the per-class AP crosses PCIe —
+        instead of every model's full [songs x thresholds] count tables down,
+        reduced and back per model. Bit-equal to threshold_map per model."""
+        import torch
+        import torch.distributed as dist
+
+        if not self._reduce():
+            return {n: self.threshold_map(t, n_thresholds) for n, t in models.items()}
+        names = list(models)
+        be = dist.get_backend(self.group)
+        host = be != "nccl"
+        dev = torch.device("cpu") if host else self.device
+        mm = []
+        for n in names:
+            mn, mx = self._minmax(models[n])
+            mm += [-mn, mx]
+        mmt = torch.tensor(mm, dtype=torch.float64, device=dev)
+        dist.all_reduce(mmt, op=dist.ReduceOp.MAX, group=self.group)
+        mmv = mmt.cpu().tolist()
+        cls, cpos = self._classes()
+        cdev = self.device if torch.cuda.is_available() else torch.device("cpu")
+        counts = torch.empty((len(names), 2, cls.shape[0], n_thresholds), dtype=torch.int32, device=cdev)
+        for i, n in enumerate(names):
+            mn, mx = -mmv[2 * i], mmv[2 * i + 1]
+            if not (mn <= mx):
+                raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
+            self._after_torch()
+            self.e.eval_class_counts(models[n].data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, cls,
+                                     counts[i].data_ptr(), n_thresholds=n_thresholds)
+        red = counts.cpu() if host and counts.is_cuda else counts
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        if red is not counts:
+            counts.copy_(red)
+        self._after_torch()  # the reduced block, written on torch's stream
+        return {n: self.e.eval_map_counts(counts[i].data_ptr(), cpos, self.n_label_songs,
+                                          n_thresholds=n_thresholds) for i, n in enumerate(names)}
 
     def topk(self, t) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Top-k recommendation lists of a dense device model (k = engine topk)."""

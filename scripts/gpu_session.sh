@@ -79,6 +79,14 @@ case ",$STEPS," in *,prof,*)
 esac
 case ",$STEPS," in *,c4,*) run bench_c4 900 python -u bench.py --config c4 --steps 5 --warmup 2 ;; esac
 case ",$STEPS," in *,c5,*) run bench_c5 900 python -u bench.py --config c5 --steps 3 --warmup 1 ;; esac
+# C5 per-model layouts (sharding.EnsembleScorer): every rank's slice on this GPU (C5N="8 4 2")
+case ",$STEPS," in *,c5models,*) run c5_models 900 python -u scripts/c5_layout_probe.py ${C5N:-8} ;; esac
+# the driver's C5 command at N ranks over gloo on this one GPU (per-model layouts, the all-to-all through the host)
+case ",$STEPS," in *,c5rehearse,*)
+  MR_BENCH_BACKEND=gloo MR_BENCH_DEVICE=0 PYTHONUNBUFFERED=1 run c5_rehearse_n2 900 python -m torch.distributed.run \
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config c5 \
+    --steps 2 --warmup 1 --no-cpu-baseline ;;
+esac
 # C4 per ItemBasedModel route (mr_options.ibm_route): ROUTES="cooc two_hop", kernels only
 case ",$STEPS," in *,c4route,*)
   for r in ${ROUTES:-cooc two_hop}; do

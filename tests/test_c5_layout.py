@@ -1,0 +1,218 @@
+"""C5's per-model layouts over N ranks, host side (gloo, world 2 and 4, no GPU):
+sharding.EnsembleScorer — ubm by test-user blocks (Spark strategy 1,
+distributed.scala:450-452), ibm by song shards (strategy 2, :477-479), ONE
+all-to-all moving the ibm shard's rows into the user-block layout, the three
+combinations on the blocks (main.scala:57-89, MR:317-481) and the five
+threshold mAPs through DeviceEnsemble.threshold_maps (one MAX and one SUM
+all-reduce of a class-indexed count block, MR:521-639).
+
+The contexts are host stand-ins holding the committed literal models of a
+fixture (tests/golden/synth_small.npz, made by oracle/reference_py.py): they
+return the rows / columns a real context scores, combine them with the numpy
+restatement of MR:317-481 at the pair indices their DeviceEnsemble hands them,
+and count with evaluation.threshold_counts. So this checks the layout itself
+— the exchange's splits and placement, pair_base of every block, the class
+layout of the reductions — against one context, bitwise; the same layout
+with the HIP engine runs in tests/test_gpu_c5_layout.py."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from musicrecommendation_amd import evaluation
+from musicrecommendation_amd.ensemble import eval_map
+from musicrecommendation_amd.sharding import EnsembleScorer
+
+from helpers import pair_index, reference_combination, synth_fixture
+
+
+def _view(ptr, n, dtype):
+    ct = {np.float64: ctypes.c_double, np.int32: ctypes.c_int32}[dtype]
+    return np.ctypeslib.as_array((ct * n).from_address(ptr))
+
+
+class HostContext:
+    """One engine context (a user block over songs [lo, hi)) over the
+    fixture's literal models: the calls EnsembleScorer / DeviceEnsemble make."""
+
+    def __init__(self, ds, *, full, models, user_lo, device=0, out_dtype="f64", topk=10, song_lo=0, song_hi=0,
+                 ibm_route="auto"):
+        self.dataset, self.full, self.models = ds, full, models
+        self.user_lo = user_lo
+        self.song_lo, self.song_hi = song_lo, song_hi or ds.n_songs
+        self.dtype, self.n_test, self.width = np.float64, ds.n_test, self.song_hi - self.song_lo
+        self.ibm_route, self.stream, self.last = "host", 0, None
+
+        class _O:
+            pass
+        self.opt = _O()
+        self.opt.device = device
+
+    def _rows(self, name):
+        m = self.models[name][self.user_lo:self.user_lo + self.n_test, self.song_lo:self.song_hi]
+        return np.ascontiguousarray(m, dtype=np.float64)
+
+    def run_into(self, name, ptr):
+        _view(ptr, self.n_test * self.width, np.float64)[:] = self._rows(name).reshape(-1)
+        self.last = name
+
+    def sync(self):
+        pass
+
+    def dense_minmax(self):
+        v = self._rows(self.last)
+        v = v[~np.isnan(v)]
+        return (float(v.min()), float(v.max())) if v.size else (np.inf, -np.inf)
+
+    def eval_minmax(self, ptr):
+        v = _view(ptr, self.n_test * self.width, np.float64)
+        v = v[~np.isnan(v)]
+        return (float(v.min()), float(v.max())) if v.size else (np.inf, -np.inf)
+
+    def combine_all(self, alpha, pct, prob, u_ptr, i_ptr, out_ptrs, *, seed, pair_base, n_pairs):
+        n = self.n_test * self.width
+        ubm = _view(u_ptr, n, np.float64).reshape(self.n_test, self.width).copy()
+        ibm = _view(i_ptr, n, np.float64).reshape(self.n_test, self.width).copy()
+        idx = pair_index(self.dataset, self.song_lo, self.song_hi, pair_base=pair_base)
+        mms = []
+        for kind, p, ptr in (("linear", alpha, out_ptrs[0]), ("aggregation", pct, out_ptrs[1]),
+                             ("stochastic", prob, out_ptrs[2])):
+            o = reference_combination(kind, ubm, ibm, p, idx, n_pairs, seed=seed)
+            _view(ptr, n, np.float64)[:] = o.reshape(-1)
+            v = o[~np.isnan(o)]
+            mms.append((float(v.min()), float(v.max())) if v.size else (np.inf, -np.inf))
+        return mms
+
+    def eval_class_counts(self, ptr, mn, mx, lab_off, lab_songs, classes, counts_ptr, n_thresholds=10):
+        ths = evaluation.THRESHOLDS if n_thresholds == 10 else evaluation.THRESHOLDS_DISTRIBUTED
+        dense = np.full((self.n_test, self.dataset.n_songs), np.nan)
+        dense[:, self.song_lo:self.song_hi] = _view(ptr, self.n_test * self.width, np.float64).reshape(
+            self.n_test, self.width)
+        p, t = evaluation.threshold_counts(dense, self.dataset, mn, mx, ths)
+        inside = (classes >= self.song_lo) & (classes < self.song_hi)
+        blk = np.zeros((2, classes.shape[0], n_thresholds), dtype=np.int32)
+        blk[0][inside], blk[1][inside] = p[classes[inside]], t[classes[inside]]
+        _view(counts_ptr, blk.size, np.int32)[:] = blk.reshape(-1)
+
+    def eval_map(self, ptr, mn, mx, lab_off, lab_songs, pos, n_label_songs, n_thresholds=10):
+        """One context holding every test user (N = 1): the whole table's fold."""
+        ths = evaluation.THRESHOLDS if n_thresholds == 10 else evaluation.THRESHOLDS_DISTRIBUTED
+        dense = _view(ptr, self.n_test * self.width, np.float64).reshape(self.n_test, self.width)
+        p, t = evaluation.threshold_counts(dense, self.dataset, mn, mx, ths)
+        return eval_map(p, t, pos, n_label_songs)
+
+    def eval_map_counts(self, counts_ptr, class_pos, n_label_songs, n_thresholds=10):
+        n = class_pos.shape[0]
+        c = _view(counts_ptr, 2 * n * n_thresholds, np.int32).reshape(2, n, n_thresholds)
+        return eval_map(c[0], c[1], class_pos, n_label_songs)
+
+    def close(self):
+        pass
+
+
+def _factory(full, models):
+    def make(ds, **kw):
+        return HostContext(ds, full=full, models=models, user_lo=_first_user(full, ds), **kw)
+    return make
+
+
+def _first_user(full, ds):
+    """Where a block's dataset (subset_test_users) starts in the full one."""
+    if ds is full or ds.n_test == full.n_test:
+        return 0
+    names = [full.test_names(i) for i in range(full.n_test)]
+    return names.index(ds.test_names(0))
+
+
+def _run(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full, z = synth_fixture("small")
+        models = {"ubm": z["ubm"], "ibm": z["ibm"]}
+        sc = EnsembleScorer(full, rank, world, 0, out_dtype="f64", engine_factory=_factory(full, models))
+        blocks, maps = sc.step(0.3, 0.4, 0.6, seed=5)
+        out[rank] = ({k: v.numpy().tolist() for k, v in blocks.items()}, maps, (sc.user_lo, sc.user_hi),
+                     sc.exchange_bytes)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _single():
+    out = {}
+    _run(0, 1, 0, out)
+    return out[0]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_per_model_layouts_equal_one_context(world):
+    one_blocks, one_maps, _, _ = _single()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_run, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    for name, full_rows in one_blocks.items():
+        full_rows = np.array(full_rows)
+        got = np.concatenate([np.array(res[r][0][name]) for r in range(world)])
+        assert np.array_equal(got, full_rows, equal_nan=True), name
+    for r in range(world):
+        assert res[r][1] == one_maps  # all five mAPs on every rank, bit for bit
+        assert res[r][3] > 0
+    assert [res[r][2] for r in range(world)] == [(full_rows.shape[0] * b // world, full_rows.shape[0] * (b + 1) // world)
+                                                 for b in range(world)]
+
+
+def test_one_context_matches_the_reference_restatement():
+    """N = 1 through the same calls = the numpy restatement of MR:317-481 and
+    the threshold mAP of MR:521-639 over the fixture's literal models."""
+    full, z = synth_fixture("small")
+    blocks, maps, _, _ = _single()
+    idx = pair_index(full)
+    ref = {"ubm": z["ubm"], "ibm": z["ibm"],
+           "lcm": reference_combination("linear", z["ubm"], z["ibm"], 0.3, idx, full.n_pairs()),
+           "am": reference_combination("aggregation", z["ubm"], z["ibm"], 0.4, idx, full.n_pairs()),
+           "scm": reference_combination("stochastic", z["ubm"], z["ibm"], 0.6, idx, full.n_pairs(), seed=5)}
+    for name, m in ref.items():
+        assert np.array_equal(np.array(blocks[name]), m, equal_nan=True), name
+        assert maps[name] == evaluation.threshold_map(m, full), name
+
+
+def test_class_count_block_sums_to_the_full_counts():
+    """The class-indexed count block of two song shards and of two user
+    blocks sums to the full table's label-class rows."""
+    full, z = synth_fixture("small")
+    dense = z["ibm"]
+    valid = ~np.isnan(dense)
+    mn, mx = dense[valid].min(), dense[valid].max()
+    p, t = evaluation.threshold_counts(dense, full, mn, mx)
+    pos = evaluation.label_pos(full)
+    cls = np.nonzero(pos > 0)[0].astype(np.int32)
+    want = np.stack([p[cls], t[cls]]).astype(np.int32)
+    models = {"ibm": dense}
+    for parts in ([dict(song_lo=0, song_hi=full.n_songs // 2), dict(song_lo=full.n_songs // 2, song_hi=0)],
+                  [dict(users=(0, full.n_test // 3)), dict(users=(full.n_test // 3, full.n_test))]):
+        total = np.zeros_like(want)
+        for kw in parts:
+            a, b = kw.pop("users", (0, full.n_test))
+            ds = full if (a, b) == (0, full.n_test) else full.subset_test_users(a, b)
+            e = HostContext(ds, full=full, models=models, user_lo=a, **kw)
+            buf = torch.empty(e.n_test * e.width, dtype=torch.float64)
+            e.run_into("ibm", buf.data_ptr())
+            blk = torch.empty((2, cls.shape[0], 10), dtype=torch.int32)
+            e.eval_class_counts(buf.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, cls, blk.data_ptr())
+            total += blk.numpy()
+        assert np.array_equal(total, want)

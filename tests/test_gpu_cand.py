@@ -97,3 +97,22 @@ def test_candidate_mode_only_for_topk_only_wide(c3_64, monkeypatch):
         assert e.shape == "fused" and not e.candidate_topk
     with Engine(c3_64, topk=10, dense=False, stage1="wide") as e:
         assert e.candidate_topk
+
+
+@pytest.mark.parametrize("nt,k,frac_bits,block", [(512, 10, 32, 8192), (512, 16, 32, 8192), (1024, 10, 40, 0),
+                                                  (512, 10, 40, 8192)])
+def test_candidate_cooc_kernel_variants(c3_64, nt, k, frac_bits, block, monkeypatch):
+    """The co-listening scoring kernel at 512 threads (NG = 32, pass A spans
+    20 x 512 songs; k up to the wide shape's 16) and the non-split dense pass of
+    frac_bits > 32, candidate-only vs all-songs vs the oracle, bitwise.
+    (MR_COOC_DS=16 is a compile-time A/B knob of the dense layout, not an
+    option of the shipped library.)"""
+    monkeypatch.setenv("MR_COOC_NT", str(nt))
+    kw = dict(frac_bits=frac_bits)
+    if block:
+        kw["block_songs"] = block
+    s1, _, k1, (lo, hi) = topk_lists(c3_64, "ibm", k, True, monkeypatch, route="cooc", **kw)
+    s0, _, k0, _ = topk_lists(c3_64, "ibm", k, False, monkeypatch, route="cooc", **kw)
+    assert np.array_equal(s1, s0) and np.array_equal(k1, k0)
+    _, ts, tk = native.fp_model(c3_64, "ibm", song_lo=lo, song_hi=hi, k=k, dense=False, frac_bits=frac_bits)
+    assert np.array_equal(s1, ts) and np.array_equal(k1, tk)

@@ -15,35 +15,9 @@ from musicrecommendation_amd.engine import Engine, merge_topk_host
 from musicrecommendation_amd.ensemble import DeviceEnsemble, pair_uniform
 from musicrecommendation_amd.sharding import song_shards
 
-from helpers import dataset_from_lines, kat, synth_fixture
+from helpers import dataset_from_lines, kat, pair_index, reference_combination, synth_fixture
 
 pytestmark = pytest.mark.gpu
-
-
-def pair_index(ds, lo=0, hi=None, user_lo=0, pair_base=0):
-    """Index of every (u, s) pair in the sorted model (NaN-free positions), or -1."""
-    hi = ds.n_songs if hi is None else hi
-    heard = ds.heard_mask()
-    idx = np.full(heard.shape, -1, dtype=np.int64)
-    run = pair_base
-    for u in range(ds.n_test):
-        free = np.flatnonzero(~heard[u])
-        idx[u, free] = run + np.arange(free.size)
-        run += free.size
-    return idx[:, lo:hi]
-
-
-def reference_combination(kind, ubm, ibm, param, idx, n_pairs, seed=0):
-    if kind == "linear":
-        return ubm * param + ibm * (1 - param)
-    if kind == "aggregation":
-        take = idx < int(param * n_pairs)
-    else:
-        u = np.vectorize(lambda i: pair_uniform(seed, int(i)) if i >= 0 else 2.0)(idx)
-        take = u < param
-    out = np.where(take, ibm, ubm)
-    out[idx < 0] = np.nan
-    return out
 
 
 def datasets():

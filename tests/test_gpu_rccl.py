@@ -39,10 +39,11 @@ def _free_port():
 
 
 @pytest.fixture
-def rccl_group():
-    """A one-rank RCCL group on cuda:0, as bench.py main() creates it."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_free_port())
+def rccl_group(monkeypatch):
+    """A one-rank RCCL group on cuda:0, as bench.py main() creates it (the
+    rendezvous variables are undone at teardown)."""
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
