@@ -395,23 +395,27 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
                        const int32_t* lab_songs, const int32_t* pos, int32_t n_label_songs, double* map_out,
                        int32_t n_thresholds);
 /* The multi-rank evaluation without the counts crossing PCIe (MR:541-627 over
- * a model spread across ranks — song shards, test-user blocks or both):
+ * models spread across ranks — song shards, test-user blocks or both), for
+ * n_models dense models of the context at once (dense: host array of device
+ * pointers; mn / mx: host arrays, the GLOBAL extremes of each model):
  * mr_eval_class_counts_device writes the counts of the label classes only into
  * a caller DEVICE buffer laid out by a class list every rank shares —
- * counts[0][c][t] = pred, counts[1][c][t] = tp of class c (2 x n_classes x
- * n_thresholds int32), 0 for classes outside the context's song range — so one
- * SUM all-reduce of the buffers over the ranks (RCCL) gives the counts over
- * every test user; classes: host, strictly ascending global song ids
- * (< n_songs; the songs with label count pos > 0: label-only songs are never
- * predicted and add 0 to the sum). mr_eval_map_counts_device then computes the
- * AP per class on the device from such a (reduced) buffer (class_pos: host,
- * each > 0) and the mean over n_label_songs, classes summed in song-id order —
- * bit-equal to mr_eval_map over the full counts. Both synchronous. */
-int mr_eval_class_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                                const int32_t* lab_songs, int32_t n_classes, const int32_t* classes,
-                                int32_t* counts, int32_t n_thresholds);
-int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_classes, const int32_t* class_pos, const int32_t* counts,
-                              int32_t n_label_songs, double* map_out, int32_t n_thresholds);
+ * counts[m][0][c][t] = pred, counts[m][1][c][t] = tp of class c for model m
+ * (n_models x 2 x n_classes x n_thresholds int32), 0 for classes outside the
+ * context's song range — so one SUM all-reduce of the buffers over the ranks
+ * (RCCL) gives the counts over every test user; classes: host, strictly
+ * ascending global song ids (< n_songs; the songs with label count pos > 0:
+ * label-only songs are never predicted and add 0 to the sum).
+ * mr_eval_map_counts_device then computes every model's AP per class on the
+ * device from such a (reduced) buffer (class_pos: host, each > 0) and the mean
+ * over n_label_songs into maps_out[m], classes summed in song-id order —
+ * bit-equal to mr_eval_map over the full counts. Both synchronous; one launch
+ * sequence and one host synchronisation per call, whatever n_models. */
+int mr_eval_class_counts_device(mr_ctx* ctx, int32_t n_models, const void* const* dense, const double* mn,
+                                const double* mx, const int64_t* lab_off, const int32_t* lab_songs, int32_t n_classes,
+                                const int32_t* classes, int32_t* counts, int32_t n_thresholds);
+int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_models, int32_t n_classes, const int32_t* class_pos,
+                              const int32_t* counts, int32_t n_label_songs, double* maps_out, int32_t n_thresholds);
 
 /* Kernel timing of mr_run calls made with opt.time_kernels = 1: per kernel
  * (0 = separate stage-1 kernel — neighbour lists —, 1 = the

@@ -178,9 +178,9 @@ SIGNATURES = {
     "mr_eval_map_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_void_p, c_int32,
                                    POINTER(c_double), c_int32]),
     "mr_eval_map": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_int32, POINTER(c_double), c_int32]),
-    "mr_eval_class_counts_device": (c_int, [c_void_p, c_void_p, c_double, c_double, c_void_p, c_void_p, c_int32,
-                                            c_void_p, c_void_p, c_int32]),
-    "mr_eval_map_counts_device": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, POINTER(c_double),
+    "mr_eval_class_counts_device": (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_int32, c_void_p, c_void_p, c_int32]),
+    "mr_eval_map_counts_device": (c_int, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_void_p,
                                           c_int32]),
     "mr_last_error": (c_char_p, []),
     "mr_corpus_from_tsv": (c_int, [c_char_p, c_char_p, c_char_p, POINTER(c_void_p)]),

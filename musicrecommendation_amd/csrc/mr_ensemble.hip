@@ -354,6 +354,12 @@ __global__ __launch_bounds__(kThreads) void k_eval_pred(EvalParams p) {
 #pragma unroll
       for (int t = 0; t < kThresholds; ++t) cnt[t] += x[r] >= xt[t] ? 1 : 0;  // NaN (no pair): never
   }
+  if (gridDim.y == 1) {  // one user block: this thread owns the song's counts (no zeroing, no atomics)
+#pragma unroll
+    for (int t = 0; t < kThresholds; ++t)
+      if (t < p.n_thr) p.pred[(size_t)i * p.n_thr + t] = cnt[t];
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < kThresholds; ++t)
     if (cnt[t]) atomicAdd(&p.pred[(size_t)i * p.n_thr + t], cnt[t]);
@@ -416,11 +422,6 @@ __global__ __launch_bounds__(kThreads) void k_eval_gather(int n_cls, int n_thr, 
   out[(size_t)n_cls * n_thr + j] = in ? tp[(size_t)g * n_thr + t] : 0;
 }
 
-__global__ __launch_bounds__(kThreads) void k_iota(int n, int* out) {
-  const int j = blockIdx.x * kThreads + threadIdx.x;
-  if (j < n) out[j] = j;
-}
-
 template <typename T>
 struct Tmp {  // scratch device buffer of one call, stream-ordered (pool allocator: no device sync)
   T* p = nullptr;
@@ -429,10 +430,17 @@ struct Tmp {  // scratch device buffer of one call, stream-ordered (pool allocat
 };
 
 // pred / tp counts of the shard into the device buffers d_pred / d_tp
-// ([width][n_thr], stream-ordered on the context stream; the caller frees them).
-int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                const int32_t* lab_songs, int n_thr, mr_view& v, Tmp<int>& d_pred, Tmp<int>& d_tp) {
-  if (!ctx || !dense || !lab_off) return fail(MR_E_INVALID, "null argument");
+// ([width][n_thr], stream-ordered on the context stream; the caller frees
+// them), for n_models dense models in turn: the labels are staged once, and
+// after model i's counts are queued after(i) queues what consumes them (the
+// buffers are reused by model i + 1, in stream order).
+template <typename After>
+int eval_counts(mr_ctx* ctx, int n_models, const void* const* dense, const double* mn, const double* mx,
+                const int64_t* lab_off, const int32_t* lab_songs, int n_thr, mr_view& v, Tmp<int>& d_pred,
+                Tmp<int>& d_tp, After&& after) {
+  if (!ctx || !dense || !lab_off || !mn || !mx || n_models < 1) return fail(MR_E_INVALID, "null argument");
+  for (int i = 0; i < n_models; ++i)
+    if (!dense[i]) return fail(MR_E_INVALID, "null dense model %d", i);
   if (n_thr != 10 && n_thr != 11)
     return fail(MR_E_INVALID, "%d thresholds: 10 (MR:590) or 11 (distributed.scala:395)", n_thr);
   int rc = mr_view_get(ctx, &v);
@@ -456,31 +464,40 @@ int eval_counts(mr_ctx* ctx, const void* dense, double mn, double mx, const int6
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_tp.p), std::max<size_t>(1, nc) * 4, st));
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_lu.p), lu.size() * 4, st));
   MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ls.p), ls.size() * 4, st));
-  MR_HIP(hipMemsetAsync(d_pred.p, 0, nc * 4, st));
-  MR_HIP(hipMemsetAsync(d_tp.p, 0, nc * 4, st));
   MR_HIP(hipMemcpyAsync(d_lu.p, lu.data(), lu.size() * 4, hipMemcpyHostToDevice, st));
   MR_HIP(hipMemcpyAsync(d_ls.p, ls.data(), ls.size() * 4, hipMemcpyHostToDevice, st));
-  // enough (song block x user block) workgroups to fill the chip
+  // (song block x user block) workgroups: ~1024 of them fill the chip (a
+  // thread keeps 16 rows' loads in flight); a user block per workgroup row
+  // adds its counts atomically, so split the users only when the songs alone
+  // give too few workgroups (narrow shards). One user block (the whole model
+  // of a wide shard, any user count): plain stores, no zeroing, no atomics —
+  // the atomics, not the model's bytes, were the pass's cost at a few hundred
+  // users (C5's 250-user blocks at 8 GPUs: 0.84 ms per model).
   const int sx = (width + kThreads - 1) / kThreads;
-  const int uy = std::max(1, std::min((n_te + 31) / 32, (8192 + sx - 1) / sx));
-  EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, n_thr, mn, mx, dense, d_pred.p, d_tp.p, d_lu.p,
-                d_ls.p, n_lab};
+  const int uy = std::max(1, std::min((n_te + 15) / 16, (1024 + sx - 1) / sx));
   const bool f64 = v.out_dtype == MR_OUT_F64;
-  for (int t = 0; t < n_thr; ++t) {
-    const double thr = kThrHost[t];
-    ep.xt_f[t] = level_floor<float, uint32_t>(mn, mx, thr);
-    ep.xt_d[t] = level_floor<double, uint64_t>(mn, mx, thr);
-  }
-  if (width > 0) {
-    if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
-    else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
-    MR_HIP(hipGetLastError());
-  }
-  if (n_lab > 0) {
-    const int lb = (int)((n_lab + kThreads - 1) / kThreads);
-    if (f64) hipLaunchKernelGGL(k_eval_tp<double>, dim3(lb), dim3(kThreads), 0, st, ep);
-    else hipLaunchKernelGGL(k_eval_tp<float>, dim3(lb), dim3(kThreads), 0, st, ep);
-    MR_HIP(hipGetLastError());
+  for (int i = 0; i < n_models; ++i) {
+    if (uy > 1) MR_HIP(hipMemsetAsync(d_pred.p, 0, nc * 4, st));
+    MR_HIP(hipMemsetAsync(d_tp.p, 0, nc * 4, st));
+    EvalParams ep{n_te, width, v.song_lo, (n_te + uy - 1) / uy, n_thr, mn[i], mx[i], dense[i], d_pred.p, d_tp.p,
+                  d_lu.p, d_ls.p, n_lab};
+    for (int t = 0; t < n_thr; ++t) {
+      const double thr = kThrHost[t];
+      ep.xt_f[t] = level_floor<float, uint32_t>(mn[i], mx[i], thr);
+      ep.xt_d[t] = level_floor<double, uint64_t>(mn[i], mx[i], thr);
+    }
+    if (width > 0) {
+      if (f64) hipLaunchKernelGGL(k_eval_pred<double>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+      else hipLaunchKernelGGL(k_eval_pred<float>, dim3(sx, uy), dim3(kThreads), 0, st, ep);
+      MR_HIP(hipGetLastError());
+    }
+    if (n_lab > 0) {
+      const int lb = (int)((n_lab + kThreads - 1) / kThreads);
+      if (f64) hipLaunchKernelGGL(k_eval_tp<double>, dim3(lb), dim3(kThreads), 0, st, ep);
+      else hipLaunchKernelGGL(k_eval_tp<float>, dim3(lb), dim3(kThreads), 0, st, ep);
+      MR_HIP(hipGetLastError());
+    }
+    if ((rc = after(i))) return rc;
   }
   // the label staging is freed in stream order after these kernels (Tmp)
   return MR_OK;
@@ -625,7 +642,7 @@ int mr_eval_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, 
   const int n_thr = thresholds_or_default(n_thresholds);
   mr_view v;
   Tmp<int> d_pred, d_tp;
-  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
+  int rc = eval_counts(ctx, 1, &dense, &mn, &mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp, [](int) { return 0; });
   if (rc) return rc;
   hipStream_t st = (hipStream_t)v.stream;
   const size_t nc = (size_t)(v.song_hi - v.song_lo) * n_thr;
@@ -642,7 +659,7 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
   const int n_thr = thresholds_or_default(n_thresholds);
   mr_view v;
   Tmp<int> d_pred, d_tp;
-  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
+  int rc = eval_counts(ctx, 1, &dense, &mn, &mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp, [](int) { return 0; });
   if (rc) return rc;
   hipStream_t st = (hipStream_t)v.stream;
   const int width = v.song_hi - v.song_lo;
@@ -674,36 +691,39 @@ int mr_eval_map_device(mr_ctx* ctx, const void* dense, double mn, double mx, con
   return MR_OK;
 }
 
-int mr_eval_class_counts_device(mr_ctx* ctx, const void* dense, double mn, double mx, const int64_t* lab_off,
-                                const int32_t* lab_songs, int32_t n_classes, const int32_t* classes,
-                                int32_t* counts, int32_t n_thresholds) {
+int mr_eval_class_counts_device(mr_ctx* ctx, int32_t n_models, const void* const* dense, const double* mn,
+                                const double* mx, const int64_t* lab_off, const int32_t* lab_songs, int32_t n_classes,
+                                const int32_t* classes, int32_t* counts, int32_t n_thresholds) {
   if (!counts || (n_classes > 0 && !classes) || n_classes < 0) return fail(MR_E_INVALID, "null argument");
   for (int32_t c = 1; c < n_classes; ++c)
     if (classes[c] <= classes[c - 1]) return fail(MR_E_INVALID, "classes not strictly ascending at %d", (int)c);
   const int n_thr = thresholds_or_default(n_thresholds);
   mr_view v;
-  Tmp<int> d_pred, d_tp;
-  int rc = eval_counts(ctx, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp);
-  if (rc) return rc;
-  hipStream_t st = (hipStream_t)v.stream;
-  if (n_classes > 0) {
-    Tmp<int> d_cls;
-    d_cls.st = st;
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)n_classes * 4, st));
-    MR_HIP(hipMemcpyAsync(d_cls.p, classes, (size_t)n_classes * 4, hipMemcpyHostToDevice, st));
+  Tmp<int> d_pred, d_tp, d_cls;
+  const size_t blk = (size_t)2 * n_classes * n_thr;  // one model's block
+  auto gather = [&](int i) -> int {
+    if (n_classes == 0) return 0;
+    hipStream_t st = (hipStream_t)v.stream;
+    if (!d_cls.p) {  // the class list, staged once (after eval_counts resolved the context)
+      d_cls.st = st;
+      MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)n_classes * 4, st));
+      MR_HIP(hipMemcpyAsync(d_cls.p, classes, (size_t)n_classes * 4, hipMemcpyHostToDevice, st));
+    }
     const int n = n_classes * n_thr;
     hipLaunchKernelGGL(k_eval_gather, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0, st, n_classes, n_thr,
-                       v.song_lo, v.song_hi - v.song_lo, d_cls.p, d_pred.p, d_tp.p, counts);
+                       v.song_lo, v.song_hi - v.song_lo, d_cls.p, d_pred.p, d_tp.p, counts + (size_t)i * blk);
     MR_HIP(hipGetLastError());
-    MR_HIP(hipStreamSynchronize(st));  // the host classes' staging copy has been read
-  }
-  MR_HIP(hipStreamSynchronize(st));
+    return 0;
+  };
+  int rc = eval_counts(ctx, n_models, dense, mn, mx, lab_off, lab_songs, n_thr, v, d_pred, d_tp, gather);
+  if (rc) return rc;
+  MR_HIP(hipStreamSynchronize((hipStream_t)v.stream));  // the host staging (labels, classes) has been read
   return MR_OK;
 }
 
-int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_classes, const int32_t* class_pos, const int32_t* counts,
-                              int32_t n_label_songs, double* map_out, int32_t n_thresholds) {
-  if (!ctx || !map_out || n_classes < 0 || (n_classes > 0 && (!class_pos || !counts)))
+int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_models, int32_t n_classes, const int32_t* class_pos,
+                              const int32_t* counts, int32_t n_label_songs, double* maps_out, int32_t n_thresholds) {
+  if (!ctx || !maps_out || n_models < 1 || n_classes < 0 || (n_classes > 0 && (!class_pos || !counts)))
     return fail(MR_E_INVALID, "null argument");
   for (int32_t c = 0; c < n_classes; ++c)
     if (class_pos[c] <= 0) return fail(MR_E_INVALID, "class %d has no positive (pos %d)", (int)c, (int)class_pos[c]);
@@ -715,27 +735,38 @@ int mr_eval_map_counts_device(mr_ctx* ctx, int32_t n_classes, const int32_t* cla
   if (rc) return rc;
   MR_HIP(hipSetDevice(v.device));
   hipStream_t st = (hipStream_t)v.stream;
-  std::vector<double> ap((size_t)std::max(1, n_classes));
+  const size_t nap = (size_t)n_models * n_classes;
+  std::vector<double> ap(std::max<size_t>(1, nap));
   if (n_classes > 0) {
+    // every model's classes as one launch: AP row m * n_classes + c reads
+    // model m's block, pred at [m][0][c][t], tp at [m][1][c][t] — tp is the
+    // pred pointer + n_classes * n_thr, so index the classes of model m as
+    // m * 2 * n_classes + c
+    std::vector<int32_t> cls(nap), cpos(nap);
+    for (int m = 0; m < n_models; ++m)
+      for (int c = 0; c < n_classes; ++c) {
+        cls[(size_t)m * n_classes + c] = 2 * m * n_classes + c;
+        cpos[(size_t)m * n_classes + c] = class_pos[c];
+      }
     Tmp<int> d_cls, d_cpos;
     Tmp<double> d_ap;
     d_cls.st = d_cpos.st = d_ap.st = st;
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), (size_t)n_classes * 4, st));
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cpos.p), (size_t)n_classes * 4, st));
-    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), (size_t)n_classes * 8, st));
-    MR_HIP(hipMemcpyAsync(d_cpos.p, class_pos, (size_t)n_classes * 4, hipMemcpyHostToDevice, st));
-    const int nb = (n_classes + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(k_iota, dim3(nb), dim3(kThreads), 0, st, n_classes, d_cls.p);
-    // the class-indexed block: pred at [0][c][t], tp at [1][c][t]
-    hipLaunchKernelGGL(k_eval_ap, dim3(nb), dim3(kThreads), 0, st, n_classes, n_thr, d_cls.p, d_cpos.p, counts,
-                       counts + (size_t)n_classes * n_thr, d_ap.p);
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cls.p), nap * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_cpos.p), nap * 4, st));
+    MR_HIP(hipMallocAsync(reinterpret_cast<void**>(&d_ap.p), nap * 8, st));
+    MR_HIP(hipMemcpyAsync(d_cls.p, cls.data(), nap * 4, hipMemcpyHostToDevice, st));
+    MR_HIP(hipMemcpyAsync(d_cpos.p, cpos.data(), nap * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_eval_ap, dim3((unsigned)((nap + kThreads - 1) / kThreads)), dim3(kThreads), 0, st, (int)nap,
+                       n_thr, d_cls.p, d_cpos.p, counts, counts + (size_t)n_classes * n_thr, d_ap.p);
     MR_HIP(hipGetLastError());
-    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, (size_t)n_classes * 8, hipMemcpyDeviceToHost, st));
+    MR_HIP(hipMemcpyAsync(ap.data(), d_ap.p, nap * 8, hipMemcpyDeviceToHost, st));
   }
   MR_HIP(hipStreamSynchronize(st));
-  double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
-  for (int c = 0; c < n_classes; ++c) total += ap[c];
-  *map_out = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
+  for (int m = 0; m < n_models; ++m) {
+    double total = 0.0;  // classes in song-id order, as mr_eval_map (MR:625-627)
+    for (int c = 0; c < n_classes; ++c) total += ap[(size_t)m * n_classes + c];
+    maps_out[m] = n_label_songs > 0 ? total / (double)n_label_songs : NAN;
+  }
   return MR_OK;
 }
 

@@ -287,29 +287,38 @@ class Engine:
             ctypes.byref(out), int(n_thresholds)), "mr_eval_map_device")
         return out.value
 
-    def eval_class_counts(self, dense_ptr: int, mn: float, mx: float, lab_off: np.ndarray, lab_songs: np.ndarray,
+    def eval_class_counts(self, dense_ptrs, mins, maxs, lab_off: np.ndarray, lab_songs: np.ndarray,
                           classes: np.ndarray, counts_ptr: int, n_thresholds: int = 10) -> None:
-        """The label classes' (pred, tp) counts into a device buffer of
-        2 x len(classes) x n_thresholds int32 (mr_eval_class_counts_device;
-        classes: ascending global song ids, shared by every rank; 0 for classes
-        outside this context's songs), ready for a SUM all-reduce."""
+        """The label classes' (pred, tp) counts of several dense device models
+        into one device buffer of len(dense_ptrs) x 2 x len(classes) x
+        n_thresholds int32 (mr_eval_class_counts_device; classes: ascending
+        global song ids, shared by every rank; 0 for classes outside this
+        context's songs; mins / maxs: each model's global extremes), ready for
+        ONE SUM all-reduce."""
+        n = len(dense_ptrs)
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.c_void_p(p) for p in dense_ptrs])
+        mn = np.ascontiguousarray(mins, dtype=np.float64)
+        mx = np.ascontiguousarray(maxs, dtype=np.float64)
         lab_off = np.ascontiguousarray(lab_off, dtype=np.int64)
         lab_songs = np.ascontiguousarray(lab_songs, dtype=np.int32)
         classes = np.ascontiguousarray(classes, dtype=np.int32)
         _lib.check(self._L.mr_eval_class_counts_device(
-            self._h, ctypes.c_void_p(dense_ptr), float(mn), float(mx), lab_off.ctypes.data_as(ctypes.c_void_p),
-            lab_songs.ctypes.data_as(ctypes.c_void_p), int(classes.shape[0]), classes.ctypes.data_as(ctypes.c_void_p),
-            ctypes.c_void_p(counts_ptr), int(n_thresholds)), "mr_eval_class_counts_device")
+            self._h, n, ptrs, mn.ctypes.data_as(ctypes.c_void_p), mx.ctypes.data_as(ctypes.c_void_p),
+            lab_off.ctypes.data_as(ctypes.c_void_p), lab_songs.ctypes.data_as(ctypes.c_void_p), int(classes.shape[0]),
+            classes.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(counts_ptr), int(n_thresholds)),
+            "mr_eval_class_counts_device")
 
-    def eval_map_counts(self, counts_ptr: int, class_pos: np.ndarray, n_label_songs: int,
-                        n_thresholds: int = 10) -> float:
-        """mAP from a (reduced) class-count device buffer (mr_eval_map_counts_device)."""
+    def eval_map_counts(self, n_models: int, counts_ptr: int, class_pos: np.ndarray, n_label_songs: int,
+                        n_thresholds: int = 10) -> list:
+        """Each model's mAP from a (reduced) class-count device buffer
+        (mr_eval_map_counts_device)."""
         class_pos = np.ascontiguousarray(class_pos, dtype=np.int32)
-        out = ctypes.c_double()
+        out = np.empty(int(n_models), dtype=np.float64)
         _lib.check(self._L.mr_eval_map_counts_device(
-            self._h, int(class_pos.shape[0]), class_pos.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(counts_ptr),
-            int(n_label_songs), ctypes.byref(out), int(n_thresholds)), "mr_eval_map_counts_device")
-        return out.value
+            self._h, int(n_models), int(class_pos.shape[0]), class_pos.ctypes.data_as(ctypes.c_void_p),
+            ctypes.c_void_p(counts_ptr), int(n_label_songs), out.ctypes.data_as(ctypes.c_void_p), int(n_thresholds)),
+            "mr_eval_map_counts_device")
+        return out.tolist()
 
     def timing_begin(self) -> None:
         """Open a timing window (one event on the engine stream)."""

@@ -261,23 +261,24 @@ class DeviceEnsemble:
         mmt = torch.tensor(mm, dtype=torch.float64, device=dev)
         dist.all_reduce(mmt, op=dist.ReduceOp.MAX, group=self.group)
         mmv = mmt.cpu().tolist()
+        mins, maxs = [-x for x in mmv[0::2]], mmv[1::2]
+        for mn, mx in zip(mins, maxs):
+            if not (mn <= mx):
+                raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
         cls, cpos = self._classes()
         cdev = self.device if torch.cuda.is_available() else torch.device("cpu")
         counts = torch.empty((len(names), 2, cls.shape[0], n_thresholds), dtype=torch.int32, device=cdev)
-        for i, n in enumerate(names):
-            mn, mx = -mmv[2 * i], mmv[2 * i + 1]
-            if not (mn <= mx):
-                raise ValueError("model has no pairs: min/max undefined (the reference throws here, MR:524)")
-            self._after_torch()
-            self.e.eval_class_counts(models[n].data_ptr(), mn, mx, self.ds.lab_off, self.ds.lab_songs, cls,
-                                     counts[i].data_ptr(), n_thresholds=n_thresholds)
+        self._after_torch()
+        self.e.eval_class_counts([models[n].data_ptr() for n in names], mins, maxs, self.ds.lab_off,
+                                 self.ds.lab_songs, cls, counts.data_ptr(), n_thresholds=n_thresholds)
         red = counts.cpu() if host and counts.is_cuda else counts
         dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
         if red is not counts:
             counts.copy_(red)
         self._after_torch()  # the reduced block, written on torch's stream
-        return {n: self.e.eval_map_counts(counts[i].data_ptr(), cpos, self.n_label_songs,
-                                          n_thresholds=n_thresholds) for i, n in enumerate(names)}
+        maps = self.e.eval_map_counts(len(names), counts.data_ptr(), cpos, self.n_label_songs,
+                                      n_thresholds=n_thresholds)
+        return dict(zip(names, maps))
 
     def topk(self, t) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Top-k recommendation lists of a dense device model (k = engine topk)."""

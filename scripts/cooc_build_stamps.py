@@ -38,9 +38,14 @@ tick_us = 0.01
 L = buf[loff:].reshape(-1, 8)
 print(f"shard [{lo},{hi}) tiles {nt}: light rows {len(L)}, heavy rows {cb['heavy_rows']}, "
       f"groups {cb['n_groups']} x {cb['group_tiles']} tiles")
+# a row is decoded only when every phase slot was written and the slots ascend
+# (the diagnostic kernels write slots 0-4 in order; a 0 = a phase never stamped)
+lok = (L[:, :5] > 0).all(axis=1) & (np.diff(L[:, :5], axis=1) >= 0).all(axis=1)
+if (~lok & (L[:, 0] > 0)).any():
+    print(f" light rows with incomplete stamps (dropped): {int((~lok & (L[:, 0] > 0)).sum())}")
 t_all0 = L[:, 0][L[:, 0] > 0].min() if (L[:, 0] > 0).any() else 0
-for (S, NT) in sorted({(int(a), int(b)) for a, b in L[:, 6:8] if a > 0}, reverse=True):
-    m = (L[:, 6] == S) & (L[:, 7] == NT) & (L[:, 0] > 0)
+for (S, NT) in sorted({(int(a), int(b)) for a, b in L[lok][:, 6:8] if a > 0}, reverse=True):
+    m = (L[:, 6] == S) & (L[:, 7] == NT) & lok
     x = L[m].astype(np.float64)
     ph = {"zero": x[:, 1] - x[:, 0], "walk": x[:, 2] - x[:, 1], "count": x[:, 3] - x[:, 2],
           "emit": x[:, 4] - x[:, 3]}
@@ -55,13 +60,22 @@ for (S, NT) in sorted({(int(a), int(b)) for a, b in L[:, 6:8] if a > 0}, reverse
     w = ph["walk"] * tick_us
     print(f"    walk per listener med {np.median(w / np.maximum(n, 1)) * 1e3:8.1f} ns")
 B = buf[boff:loff].reshape(-1, 8)
-B = B[B[:, 0] > 0].astype(np.float64)
+B = B[B[:, 0] > 0]
+# complete workgroups only: slots 0 <= 1 <= 3 <= 2 <= 4 all written (k_cooc_build
+# writes slot 3 = slot 2: no pass split)
+bok = (B[:, :5] > 0).all(axis=1) & (B[:, 1] >= B[:, 0]) & (B[:, 3] >= B[:, 1]) & (B[:, 2] >= B[:, 3]) & \
+    (B[:, 4] >= B[:, 2])
+if (~bok).any():
+    print(f" heavy WGs with incomplete stamps (dropped): {int((~bok).sum())}")
+B = B[bok].astype(np.float64)
 if len(B):
     dur = (B[:, 4] - B[:, 0]) * tick_us
     print(f" heavy WGs {len(B)} (big {int(B[:, 5].sum())}), span {(B[:, 4].max() - B[:, 0].min()) * tick_us / 1e3:.2f} ms, "
           f"sum(WG time)/256 {dur.sum() / 256 / 1e3:.2f} ms")
-    g = B[:, 3] >= B[:, 1]  # group-kernel workgroups (stamp 3: the first group's emission pass A)
-    for kind, sel in (("pipelined rows", g & (B[:, 5] == 0)), ("big rows (row, group)", g & (B[:, 5] == 1))):
+    b32 = B[:, 7] == -1  # k_cooc_build: the u32 rows, one workgroup per (row, tile)
+    g = ~b32             # k_cooc_group (slot 7: its group count, 1 for big rows)
+    for kind, sel in (("pipelined rows", g & (B[:, 5] == 0)), ("big rows (row, group)", g & (B[:, 5] == 1)),
+                      ("u32 rows (row, tile), k_cooc_build", b32)):
         if not sel.any():
             continue
         print(f"   {kind}: WGs {sel.sum()} med {np.median(dur[sel]):8.1f} us, share {dur[sel].sum() / dur.sum():.3f}")

@@ -81,6 +81,10 @@ case ",$STEPS," in *,c4,*) run bench_c4 900 python -u bench.py --config c4 --ste
 case ",$STEPS," in *,c5,*) run bench_c5 900 python -u bench.py --config c5 --steps 3 --warmup 1 ;; esac
 # C5 per-model layouts (sharding.EnsembleScorer): every rank's slice on this GPU (C5N="8 4 2")
 case ",$STEPS," in *,c5models,*) run c5_models 900 python -u scripts/c5_layout_probe.py ${C5N:-8} ;; esac
+case ",$STEPS," in *,profc5models,*)
+  export TMPDIR=/tmp
+  run prof_c5_models 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5_models" -o p -- python3 "$ROOT/scripts/c5_layout_probe.py" ${C5N:-8} ;;
+esac
 # the driver's C5 command at N ranks over gloo on this one GPU (per-model layouts, the all-to-all through the host)
 case ",$STEPS," in *,c5rehearse,*)
   MR_BENCH_BACKEND=gloo MR_BENCH_DEVICE=0 PYTHONUNBUFFERED=1 run c5_rehearse_n2 900 python -m torch.distributed.run \

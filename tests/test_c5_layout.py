@@ -88,15 +88,16 @@ class HostContext:
             mms.append((float(v.min()), float(v.max())) if v.size else (np.inf, -np.inf))
         return mms
 
-    def eval_class_counts(self, ptr, mn, mx, lab_off, lab_songs, classes, counts_ptr, n_thresholds=10):
+    def eval_class_counts(self, ptrs, mins, maxs, lab_off, lab_songs, classes, counts_ptr, n_thresholds=10):
         ths = evaluation.THRESHOLDS if n_thresholds == 10 else evaluation.THRESHOLDS_DISTRIBUTED
-        dense = np.full((self.n_test, self.dataset.n_songs), np.nan)
-        dense[:, self.song_lo:self.song_hi] = _view(ptr, self.n_test * self.width, np.float64).reshape(
-            self.n_test, self.width)
-        p, t = evaluation.threshold_counts(dense, self.dataset, mn, mx, ths)
         inside = (classes >= self.song_lo) & (classes < self.song_hi)
-        blk = np.zeros((2, classes.shape[0], n_thresholds), dtype=np.int32)
-        blk[0][inside], blk[1][inside] = p[classes[inside]], t[classes[inside]]
+        blk = np.zeros((len(ptrs), 2, classes.shape[0], n_thresholds), dtype=np.int32)
+        for i, (ptr, mn, mx) in enumerate(zip(ptrs, mins, maxs)):
+            dense = np.full((self.n_test, self.dataset.n_songs), np.nan)
+            dense[:, self.song_lo:self.song_hi] = _view(ptr, self.n_test * self.width, np.float64).reshape(
+                self.n_test, self.width)
+            p, t = evaluation.threshold_counts(dense, self.dataset, mn, mx, ths)
+            blk[i, 0][inside], blk[i, 1][inside] = p[classes[inside]], t[classes[inside]]
         _view(counts_ptr, blk.size, np.int32)[:] = blk.reshape(-1)
 
     def eval_map(self, ptr, mn, mx, lab_off, lab_songs, pos, n_label_songs, n_thresholds=10):
@@ -106,10 +107,10 @@ class HostContext:
         p, t = evaluation.threshold_counts(dense, self.dataset, mn, mx, ths)
         return eval_map(p, t, pos, n_label_songs)
 
-    def eval_map_counts(self, counts_ptr, class_pos, n_label_songs, n_thresholds=10):
+    def eval_map_counts(self, n_models, counts_ptr, class_pos, n_label_songs, n_thresholds=10):
         n = class_pos.shape[0]
-        c = _view(counts_ptr, 2 * n * n_thresholds, np.int32).reshape(2, n, n_thresholds)
-        return eval_map(c[0], c[1], class_pos, n_label_songs)
+        c = _view(counts_ptr, n_models * 2 * n * n_thresholds, np.int32).reshape(n_models, 2, n, n_thresholds)
+        return [eval_map(c[m, 0], c[m, 1], class_pos, n_label_songs) for m in range(n_models)]
 
     def close(self):
         pass
@@ -212,7 +213,7 @@ def test_class_count_block_sums_to_the_full_counts():
             e = HostContext(ds, full=full, models=models, user_lo=a, **kw)
             buf = torch.empty(e.n_test * e.width, dtype=torch.float64)
             e.run_into("ibm", buf.data_ptr())
-            blk = torch.empty((2, cls.shape[0], 10), dtype=torch.int32)
-            e.eval_class_counts(buf.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, cls, blk.data_ptr())
-            total += blk.numpy()
+            blk = torch.empty((1, 2, cls.shape[0], 10), dtype=torch.int32)
+            e.eval_class_counts([buf.data_ptr()], [mn], [mx], ds.lab_off, ds.lab_songs, cls, blk.data_ptr())
+            total += blk.numpy()[0]
         assert np.array_equal(total, want)

@@ -70,8 +70,10 @@ def test_two_ranks_per_model_layouts_on_one_gpu(route):
 
 
 def test_class_count_reduction_equals_device_map():
-    """mr_eval_class_counts_device + mr_eval_map_counts_device on one context
-    = mr_eval_map_device (counts over every test user, no reduction)."""
+    """mr_eval_class_counts_device + mr_eval_map_counts_device over both
+    models at once on one context = mr_eval_map_device per model (counts over
+    every test user, no reduction), and the class blocks = the full tables'
+    label-class rows."""
     from musicrecommendation_amd import evaluation
     from musicrecommendation_amd.engine import Engine
     from musicrecommendation_amd.ensemble import DeviceEnsemble
@@ -81,17 +83,17 @@ def test_class_count_reduction_equals_device_map():
         ens = DeviceEnsemble(e)
         pos = evaluation.label_pos(ds)
         cls = np.nonzero(pos > 0)[0].astype(np.int32)
-        for name in ("ubm", "ibm"):
-            t = ens.model(name)
-            mn, mx = e.eval_minmax(t.data_ptr())
-            for n_thr in (10, 11):
-                want = e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, pos, ds.n_label_songs,
-                                  n_thresholds=n_thr)
-                blk = torch.empty((2, cls.shape[0], n_thr), dtype=torch.int32, device="cuda")
-                e.eval_class_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, cls, blk.data_ptr(),
-                                    n_thresholds=n_thr)
-                got = e.eval_map_counts(blk.data_ptr(), pos[cls], ds.n_label_songs, n_thresholds=n_thr)
-                assert got == want, (name, n_thr)
+        ts = [ens.model(name) for name in ("ubm", "ibm")]
+        mms = [e.eval_minmax(t.data_ptr()) for t in ts]
+        for n_thr in (10, 11):
+            want = [e.eval_map(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, pos, ds.n_label_songs,
+                               n_thresholds=n_thr) for t, (mn, mx) in zip(ts, mms)]
+            blk = torch.empty((2, 2, cls.shape[0], n_thr), dtype=torch.int32, device="cuda")
+            e.eval_class_counts([t.data_ptr() for t in ts], [m[0] for m in mms], [m[1] for m in mms], ds.lab_off,
+                                ds.lab_songs, cls, blk.data_ptr(), n_thresholds=n_thr)
+            got = e.eval_map_counts(2, blk.data_ptr(), pos[cls], ds.n_label_songs, n_thresholds=n_thr)
+            assert got == want, n_thr
+            b = blk.cpu().numpy()
+            for i, (t, (mn, mx)) in enumerate(zip(ts, mms)):
                 p, tp = e.eval_counts(t.data_ptr(), mn, mx, ds.lab_off, ds.lab_songs, n_thresholds=n_thr)
-                b = blk.cpu().numpy()
-                assert np.array_equal(b[0], p[cls]) and np.array_equal(b[1], tp[cls])
+                assert np.array_equal(b[i, 0], p[cls]) and np.array_equal(b[i, 1], tp[cls])

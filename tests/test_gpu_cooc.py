@@ -255,3 +255,31 @@ def test_cooc_stats_count_the_index(build_path):
     else:  # a test dense rule charges a sparse-enough dense segment its tile's songs
         assert got_index >= int(seg_min.sum())
         assert cb["consumed_bytes"] >= int((seg_min * users_r).sum())
+
+
+@pytest.mark.parametrize("n_listeners,n_common", [(100, 5), (700, 9), (2000, 13)])
+def test_light_rows_shared_songs_and_straddling_chunks(n_listeners, n_common, monkeypatch):
+    """The light rows' LDS hash insert (light_insert_queue, MR:232-235's
+    counts): every listener of the row holds the same n_common songs, so
+    hundreds of lanes claim and add to the same slots at once (CAS-first, then
+    an add on a tag match), and the listeners' rows have every length mod 8,
+    so a lane's 16-B chunk often ends inside a listener's row with the NEXT
+    listener's songs right behind it in sr_songs — the key batch a lane hands
+    over is a prefix of m < 8 valid keys of ONE listener (distinct songs) and
+    no key past m may be inserted (the invariant the reverted two-queue insert
+    of r05 s43 broke). Counts up to 2000 per slot (< the 4095
+    the 12 count bits hold; mr_load keeps rows with more listeners off the
+    light path). Dense scores and top-k bitwise vs the oracle."""
+    monkeypatch.delenv("MR_COOC_LIGHT", raising=False)
+    tr, te = [], []
+    for v in range(n_listeners):
+        songs = ["hub"] + [f"c{j:02d}" for j in range(n_common)] + [f"p{v:05d}_{j}" for j in range(v % 8)]
+        tr += [f"v{v:05d}\t{s}\t1" for s in songs]
+    te = ["x0\thub\t1", "x1\tc00\t1", "x2\thub\t1", "x2\tp00003_1\t1", "x3\tp00007_6\t1"]
+    from helpers import dataset_from_lines
+    ds = dataset_from_lines(tr, te, [])
+    for k in (1, 10):
+        check_route_exact(ds, k=k)
+    with Engine(ds, out_dtype="f64", topk=10, stage1="wide", ibm_route="cooc") as e:
+        e.run("ibm")
+        assert e.cooc_bytes()["light_rows"] >= 1  # the rows went through the hash tables
