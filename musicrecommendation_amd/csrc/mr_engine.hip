@@ -1083,15 +1083,7 @@ struct ScoreParams {
   int topk_lists;                // 1: skip the threshold top-k (mr_options.topk_lists)
   // co-listening route (wide shape, ibm; k_cooc_build's index)
   int n_rows, nseg;              // index rows; segment descriptors per LDS pass
-  const int* te_row;             // per te_songs entry: its index row, -1 = none (no train listener,
-                                 //   or a listener-list row, below)
-  // listener-list rows (MR_COOC_HL): light rows read by few test users are not
-  // built; the user's workgroups walk their listeners' tile segments instead
-  // (the two-hop stage 2 over tsongs, weight q(s2) per (row, listener)):
-  // user u's (listener, q) pairs at [hl_off[u], hl_off[u+1]), or null
-  const long long* hl_off;
-  const int* hl_v;
-  const unsigned long long* hl_q;
+  const int* te_row;             // per te_songs entry: its index row, -1 = no train listener
   const long long* seg_off;      // [tile][row]: first pool entry of the row's tile segment
   const int* seg_len;            // [tile][row]: its entries
   const unsigned* pool;          // entries (tile-local song << kCoocCntBits) | C[s2][s]
@@ -1673,9 +1665,6 @@ typedef unsigned short us2_t __attribute__((ext_vector_type(2)));
 #endif
 #ifndef MR_COOC_P16
 #define MR_COOC_P16 1       // 0: every heavy row with u32 counters (A/B)
-#endif
-#ifndef MR_COOC_HL_R
-#define MR_COOC_HL_R 2      // co-listening scoring: listener-list rows' listeners per thread per iteration
 #endif
 #ifndef MR_COOC_NT
 #define MR_COOC_NT 1024     // co-listening index build: threads per workgroup
@@ -2272,27 +2261,6 @@ __global__ __launch_bounds__(NT) void k_score_wide(ScoreParams p) {
       }
       __syncthreads();  // the next pass rewrites the descriptors
       MR_STAMP(14);  // sparse segments walked
-    }
-    // listener-list rows: their (listener, q(s2)) pairs' tile segments,
-    // acc[s] += q(s2) per entry — C[s2][s] * q(s2) summed one listener at a
-    // time, the same integer sum as the index rows' (MR:232-235, MR:251-253)
-    if (p.hl_off) {
-      const long long h0 = p.hl_off[u];
-      const int hn = (int)(p.hl_off[u + 1] - h0);
-      if (hn > 0) {
-        constexpr int RH = MR_COOC_HL_R;
-        auto load_hl = [&](int k0, int (&v)[RH], unsigned long long (&q)[RH]) {
-#pragma unroll
-          for (int r = 0; r < RH; ++r) {
-            const int k = k0 + r * NT;
-            v[r] = k < hn ? p.hl_v[h0 + k] : -1;
-            q[r] = k < hn ? p.hl_q[h0 + k] : 0ull;
-          }
-        };
-        walk_tile_lists<NT, RH, MR_WIDE_SEG, unsigned long long>(
-            tid, hn, load_hl, p.toff + (size_t)tile * p.n_tr, p.tsongs,
-            [&](unsigned x, unsigned long long q) { atomicAdd(&acc[x], q); });
-      }
     }
   } else {
   // stage 2: R neighbours per thread in flight; each segment's first kSeg
@@ -3864,11 +3832,6 @@ struct mr_ctx {
   DevBuf<unsigned> urec;           // k_cooc_group: per-user tile starts (load-time only: lrec's source)
   DevBuf<unsigned> lrec;           // k_cooc_group: per-(row, listener) base + tile-group starts
   DevBuf<uint2> llrec;             // k_cooc_light*: per-(row, listener) shard-row ranges
-  DevBuf<long long> hl_off;        // listener-list rows (MR_COOC_HL): per test user, its pairs' start
-  DevBuf<int> hl_v;                //   the pairs' train listeners
-  DevBuf<unsigned long long> hl_q; //   and their rows' weights q(s2)
-  long long n_hl = 0;              // (listener, q) pairs over the context's test users
-  std::vector<uint8_t> row_hl;     // per row: a listener-list row (not built)
   int grp = 0, n_grp = 0, urec_words = 0, lrec_words = 0;
   int group_nt = 1024;             // threads per k_cooc_group workgroup (MR_COOC_GNT)
 
@@ -3888,8 +3851,7 @@ struct mr_ctx {
     pool.release();
     rows_order.release(); row_slots.release(); sr_off.release(); sr_songs.release(); row_nnz.release();
     urec.release(); lrec.release(); llrec.release(); rdesc.release(); grp = n_grp = urec_words = lrec_words = 0;
-    row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear(); row_hl.clear();
-    hl_off.release(); hl_v.release(); hl_q.release(); n_hl = 0;
+    row_users.clear(); row_reads.clear(); row_listeners.clear(); row_light.clear();
     build_reads = 0; cooc_ran = false;
     ibm_route = 1; n_rows = 0; nseg = 0; pool_cap = 0; cooc_kernel = nullptr; n_heavy = n_light = n_heavy32 = 0;
     for (int& x : n_light_tier) x = 0;
@@ -4002,14 +3964,6 @@ int64_t cooc_light_load_opt() {
 bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
   return !(e && std::atoi(e) == 0);
-}
-// Listener-list rows (MR_COOC_HL=T): light rows whose song is visible to at
-// most T test users of the context are not built; their users' scoring
-// workgroups walk the rows' listeners' tile segments instead (0 = off: every
-// row built). Read at each mr_load.
-int cooc_hl_opt() {
-  const char* e = std::getenv("MR_COOC_HL");
-  return e ? std::max(0, std::atoi(e)) : 0;
 }
 // Heavy u16 rows by tile groups (k_cooc_group, default) or per tile
 // (MR_COOC_GROUP=0: k_cooc_build<512, true>; A/B experiments and tests; read
@@ -4542,7 +4496,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   std::vector<int32_t> row_song, te_row;
   std::vector<int64_t> row_base;
   std::vector<int32_t> heavy_rows, light_rows, row_slots;
-  std::vector<uint8_t> row_hl;  // listener-list rows (cooc_hl_opt)
   int dense_div = kCoocDenseDiv;
   int n_heavy32 = 0, n_big16 = 0, tcap16 = 0, tcap32 = 0;
   int32_t max_shard_deg = 0;
@@ -4641,18 +4594,8 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       // the scorer's dvec_t loads and k_cooc_group's chunk_t stores
       dense_pad = (dense_pad + 3) & ~(int64_t)3;
       row_slots.assign((size_t)std::max<int64_t>(1, nr), 0);
-      // test users per row (a song is in T(u) at most once)
-      const int hl_max = cooc_hl_opt();
-      std::vector<int32_t> row_te((size_t)std::max<int64_t>(1, nr), 0);
-      for (int64_t i = 0; i < d->te_off[n_te]; ++i)
-        if (te_row[i] >= 0) row_te[te_row[i]]++;
-      row_hl.assign((size_t)std::max<int64_t>(1, nr), 0);
       for (int64_t r = 0; r < nr; ++r) {
-        if (light_ok && hl_max > 0 && row_te[r] <= hl_max && row_base[r] * 100 <= light_slots_max * lload &&
-            col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
-          row_hl[r] = 1;  // a listener-list row: no pool range, no build
-          row_base[r] = 0;
-        } else if (light_ok && row_base[r] * 100 <= light_slots_max * lload && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
+        if (light_ok && row_base[r] * 100 <= light_slots_max * lload && col_tr[row_song[r]] <= (int32_t)kLightCntMask) {
           int sl = 1024;
           while ((int64_t)sl * lload < row_base[r] * 100) sl <<= 1;
           row_slots[r] = sl;
@@ -4807,43 +4750,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
   }  // (separate / wide shapes: neighbour lists allocated by the first two-hop run, ensure_nbr)
   if (route == 2) {
     const size_t nr = row_song.size();
-    // listener-list rows: each test user's (listener, q(s2)) pairs of its
-    // songs on such rows (the transpose's listener ranges laid end to end,
-    // as te_rng / llrec resolve them at load), and their te_row entries
-    // dropped from the index passes
-    c->n_hl = 0;
-    if (std::find(row_hl.begin(), row_hl.end(), (uint8_t)1) != row_hl.end()) {
-      std::vector<long long> ho((size_t)n_te + 1, 0);
-      for (int u = 0; u < n_te; ++u) {
-        long long n = 0;
-        for (int64_t i = d->te_off[u]; i < d->te_off[u + 1]; ++i)
-          if (te_row[i] >= 0 && row_hl[te_row[i]]) n += col_tr[d->te_songs[i]];
-        ho[u + 1] = ho[u] + n;
-      }
-      const long long nh = ho[n_te];
-      std::vector<int32_t> hv((size_t)std::max<long long>(1, nh));
-      std::vector<unsigned long long> hq((size_t)std::max<long long>(1, nh));
-      mr_par::parallel_for(n_te, [&](int64_t a, int64_t b, int) {
-        for (int64_t u = a; u < b; ++u) {
-          long long o = ho[u];
-          for (int64_t i = d->te_off[u]; i < d->te_off[u + 1]; ++i) {
-            if (te_row[i] < 0 || !row_hl[te_row[i]]) continue;
-            const int s2 = d->te_songs[i];
-            for (int64_t j = trs_off[s2]; j < trs_off[s2 + 1]; ++j, ++o) {
-              hv[o] = trs_users[j];
-              hq[o] = (unsigned long long)q_song[s2];
-            }
-          }
-        }
-      });
-      for (int64_t i = 0; i < d->te_off[n_te]; ++i)
-        if (te_row[i] >= 0 && row_hl[te_row[i]]) te_row[i] = -1;
-      if ((rc = dev_upload(c->hl_off, ho.data(), ho.size(), st))) return rc;
-      if ((rc = dev_upload(c->hl_v, hv.data(), hv.size(), st))) return rc;
-      if ((rc = dev_upload(c->hl_q, hq.data(), hq.size(), st))) return rc;
-      MR_HIP(hipStreamSynchronize(st));  // hv / hq die here
-      c->n_hl = nh;
-    }
     if ((rc = dev_upload(c->row_song, row_song.data(), nr, st))) return rc;
     if ((rc = dev_upload(c->te_row, te_row.data(), te_row.size(), st))) return rc;
     if ((rc = dev_upload(c->row_base, reinterpret_cast<const long long*>(row_base.data()), nr + 1, st))) return rc;
@@ -4989,8 +4895,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->cooc_lds = (size_t)cooc_build_lds<false>(bs);
     c->n_heavy = (int)heavy_rows.size();
     c->build_reads = 0;
-    for (size_t r = 0; r < row_reads.size(); ++r)
-      if (r >= row_hl.size() || !row_hl[r]) c->build_reads += row_reads[r];
+    for (int64_t x : row_reads) c->build_reads += x;
     c->row_users.assign(row_song.size(), 0);
     for (size_t i = 0; i < (size_t)d->te_off[n_te]; ++i)
       if (te_row[i] >= 0) c->row_users[te_row[i]]++;
@@ -4999,8 +4904,6 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     for (size_t r = 0; r < row_song.size(); ++r) c->row_listeners[r] = col_tr[row_song[r]];
     c->row_light.assign(row_song.size(), 0);
     for (int32_t r : light_rows) c->row_light[r] = 1;
-    c->row_hl = row_hl;
-    c->row_hl.resize(row_song.size(), 0);
     c->n_heavy32 = n_heavy32;
     c->n_big16 = n_big16;
     c->grp = grp;
@@ -5106,7 +5009,6 @@ int mr_cooc_bytes(mr_ctx* c, mr_cooc_bytes_t* out) {
   MR_HIP(hipStreamSynchronize(c->stream));
   mr_cooc_bytes_t b{};
   for (int r = 0; r < nr; ++r) {
-    if (!c->row_hl.empty() && c->row_hl[r]) continue;  // a listener-list row: no index segments
     int64_t seg = 0;  // Σ_t min(4 nnz(r, t), songs of t)
     int64_t sp = 0, ds = 0;  // the written encoding: sparse entries, dense songs
     for (int t = 0; t < nt; ++t) {
@@ -5322,10 +5224,6 @@ int run_cooc(mr_ctx* c) {
     sp.sqrt_c = c->sqrt_c.p; sp.q_song = c->q_song.p;
     sp.n_rows = c->n_rows; sp.nseg = c->nseg;
     sp.te_row = c->te_row.p; sp.seg_off = c->seg_off.p; sp.seg_len = c->seg_len.p; sp.pool = c->pool.p;
-    if (c->n_hl > 0) {  // listener-list rows: the tile-major train CSR's segments
-      sp.hl_off = c->hl_off.p; sp.hl_v = c->hl_v.p; sp.hl_q = c->hl_q.p;
-      sp.toff = c->toff.p; sp.tsongs = c->tsongs.p;
-    }
     sp.dense_out = c->dense_override ? c->dense_override : (void*)c->dense.p;
     sp.cand_key = c->cand_key.p; sp.cand_song = c->cand_song.p; sp.counter = c->counter.p;
     sp.top_key = c->top_key.p; sp.top_song = c->top_song.p; sp.top_score = c->top_score.p;
