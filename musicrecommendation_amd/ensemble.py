@@ -9,9 +9,12 @@ the per-class confusion counts and the top-k run as HIP kernels
 on the host over the integer counts (mr_eval_map).
 
 Multi-GPU: every rank holds one engine context (a song shard or a block of
-test users). min/max are all-reduced (MIN/MAX), the counts are all-reduced
-(SUM) into a full n_songs x 10 table, so every rank computes the same mAP,
-bit for bit, for any shard count.
+test users). threshold_map all-reduces min/max (MIN/MAX) and the counts
+(SUM) into a full n_songs x 10 table per model; threshold_maps does several
+models at once with one MAX all-reduce of their (-min, max) and one SUM
+all-reduce of a class-indexed count block built and folded on the device
+(mr_eval_class_counts_device / mr_eval_map_counts_device). Either way every
+rank computes the same mAP, bit for bit, for any layout.
 """
 from __future__ import annotations
 

@@ -310,7 +310,7 @@ class EnsembleScorer:
         from .engine import Engine
         from .ensemble import DeviceEnsemble
 
-        Engine = engine_factory or Engine  # noqa: N806  (tests: host stand-ins of the contexts)
+        make = engine_factory or Engine  # (tests: host stand-ins of the contexts)
 
         self.full, self.rank, self.world, self.group = full, rank, world, group
         self.blocks = user_blocks(full.n_test, world)
@@ -323,11 +323,11 @@ class EnsembleScorer:
         self.ds_u = full if world == 1 else full.subset_test_users(self.user_lo, self.user_hi)
         # the block's context scores ubm over all songs (no co-listening pool:
         # its ibm is never run when N > 1)
-        self.eng_u = Engine(self.ds_u, device=device, out_dtype=out_dtype, topk=topk,
-                            ibm_route=ibm_route if world == 1 else "two_hop")
-        self.eng_i = self.eng_u if world == 1 else Engine(full, device=device, out_dtype=out_dtype, topk=topk,
-                                                           song_lo=self.song_lo, song_hi=self.song_hi,
-                                                           ibm_route=ibm_route)
+        self.eng_u = make(self.ds_u, device=device, out_dtype=out_dtype, topk=topk,
+                          ibm_route=ibm_route if world == 1 else "two_hop")
+        self.eng_i = self.eng_u if world == 1 else make(full, device=device, out_dtype=out_dtype, topk=topk,
+                                                         song_lo=self.song_lo, song_hi=self.song_hi,
+                                                         ibm_route=ibm_route)
         kw = dict(n_pairs=full.n_pairs(), pos=pos, n_label_songs=full.n_label_songs, group=group,
                   collectives=collectives)
         self.ens = DeviceEnsemble(self.eng_u, pair_base=a * full.n_songs - int(full.te_off[a]), **kw)
