@@ -113,6 +113,13 @@ def test_threshold_map_reductions_over_rccl(rccl_group):
                 assert red.threshold_map(t, nt) == loc.threshold_map(t, nt)
         exp = evaluation.threshold_map(lcm.cpu().numpy().astype(np.float64), ds)
         assert abs(red.threshold_map(lcm) - exp) <= 1e-12
+        # the batched path of the multi-rank C5 step: one MAX all-reduce of
+        # the five (-min, max), the class-indexed count block of all five
+        # models SUM-all-reduced over RCCL on the device, the AP on the device
+        models = {"ubm": u, "ibm": i, "lcm": lcm, "am": am, "scm": scm}
+        for nt in (10, 11):
+            got = red.threshold_maps(models, nt)
+            assert got == {n: loc.threshold_map(t, nt) for n, t in models.items()}
 
 
 def test_bench_one_rank_rccl_rehearsal(tmp_path):
@@ -140,3 +147,28 @@ def test_bench_one_rank_rccl_rehearsal(tmp_path):
     assert ns["ms_per_step"] > 0 and ns["layout"] == "songs1xusers1"
     # the temporary hand-off directory of shared_bulk_dataset was removed
     assert not [d for d in os.listdir(tmp_path) if d.startswith("mr_")]
+
+
+def test_bench_c5_one_rank_rccl_rehearsal(tmp_path):
+    """The C5 line under torchrun at N = 1 with MR_BENCH_PG=1: the process
+    group up over RCCL, shared_bulk_dataset's hand-off, EnsembleScorer and
+    DeviceEnsemble.threshold_maps' MAX and SUM all-reduces of the five
+    models' extremes and class-count block over RCCL — the same five mAPs
+    as the single-process line computes without collectives."""
+    env = dict(os.environ, MR_BENCH_PG="1", TMPDIR=str(tmp_path), PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--config", "c5", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-e2e"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    maps = line["threshold_mAP"]
+    assert set(maps) == {"ubm", "ibm", "lcm", "am", "scm"} and all(0 < v < 1 for v in maps.values())
+    # the single-process line's values on the same seeded data (every C5 bench
+    # of rounds 5-6, e.g. profiles/r06/bench_c5.json): a regression anchor of
+    # this engine's own output, not a reference fixture
+    ref = {"ubm": 0.0009340961307245022, "ibm": 0.0020751807777950114, "lcm": 0.0009403874247581429,
+           "am": 0.0009064927680186897, "scm": 0.0008915149560019554}
+    assert maps == ref
