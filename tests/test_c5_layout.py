@@ -159,8 +159,10 @@ def _single():
     return out[0]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_gloo_per_model_layouts_equal_one_context(world):
+    """(world 3: uneven user blocks and song shards, so the all-to-all's
+    splits differ per rank pair)"""
     one_blocks, one_maps, _, _ = _single()
     with mp.Manager() as m:
         out = m.dict()
