@@ -742,6 +742,8 @@ def main() -> None:
                          "(--no-graph: K stream launches)")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps per captured graph (must divide --steps; 0 = all K in one graph)")
+    ap.add_argument("--rehearse", action=argparse.BooleanOptionalAction, default=True,
+                    help="graph path: run the timed region's call sequence once, untimed, before it")
     ap.add_argument("--stream-sync", action="store_true",
                     help="close the timed region with engine-stream waits before torch.cuda.synchronize() "
                          "(default: one device-wide synchronize, the window's event read afterwards)")
@@ -847,6 +849,21 @@ def main() -> None:
     if use_graph:  # the K timed steps as K / G replays of a G-step HIP graph (captured untimed)
         eng.graph_capture(args.model, g_steps)
         eng.graph_launch()  # first replay uploads the graph: untimed
+        drain()
+    if use_graph and args.rehearse:
+        # The timed region's exact call sequence once, untimed (warmup): the
+        # first window's event records and closing synchronisation otherwise
+        # pay their first-call cost inside the only region a short run times
+        # (profiles/r06/s17-s18).
+        if _pg():
+            dist.barrier()
+        torch.cuda.synchronize()
+        eng.timing_begin()
+        for _ in range(args.steps // g_steps):
+            eng.graph_launch()
+        eng.timing_stop()
+        torch.cuda.synchronize()
+        eng.timing_end()
         drain()
     if _pg():
         dist.barrier()
