@@ -107,3 +107,11 @@ def reference_combination(kind, ubm, ibm, param, idx, n_pairs, seed=0):
     out = np.where(take, ibm, ubm)
     out[idx < 0] = np.nan
     return out
+
+
+def pg_init_method() -> str:
+    """Rendezvous of the multi-process tests: a FileStore in a fresh temporary
+    directory instead of a TCP port picked in advance (a port found free can be
+    taken by another process before the store binds it: EADDRINUSE). The
+    backends still open their own sockets on ports they bind themselves."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="mr_pg_"), "store")

@@ -16,7 +16,6 @@ layout of the reductions — against one context, bitwise; the same layout
 with the HIP engine runs in tests/test_gpu_c5_layout.py."""
 import ctypes
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -28,7 +27,7 @@ from musicrecommendation_amd import evaluation
 from musicrecommendation_amd.ensemble import eval_map
 from musicrecommendation_amd.sharding import EnsembleScorer
 
-from helpers import pair_index, reference_combination, synth_fixture
+from helpers import pair_index, pg_init_method, reference_combination, synth_fixture
 
 
 def _view(ptr, n, dtype):
@@ -130,11 +129,9 @@ def _first_user(full, ds):
     return names.index(ds.test_names(0))
 
 
-def _run(rank, world, port, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
+def _run(rank, world, init, out):
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         full, z = synth_fixture("small")
         models = {"ubm": z["ubm"], "ibm": z["ibm"]}
@@ -145,12 +142,6 @@ def _run(rank, world, port, out):
     finally:
         if world > 1:
             dist.destroy_process_group()
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _single():
@@ -166,7 +157,7 @@ def test_gloo_per_model_layouts_equal_one_context(world):
     one_blocks, one_maps, _, _ = _single()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_run, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_run, args=(world, pg_init_method(), out), nprocs=world, join=True)
         res = dict(out)
     for name, full_rows in one_blocks.items():
         full_rows = np.array(full_rows)

@@ -5,22 +5,15 @@ all-to-all, the combinations on the blocks and the five threshold mAPs through
 the class-count reduction (mr_eval_class_counts_device +
 mr_eval_map_counts_device). Every model's rows and every mAP equal one
 context's, bitwise, on both ibm routes."""
-import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import pg_init_method
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _dataset():
@@ -28,13 +21,11 @@ def _dataset():
     return synth.config("c3", n_test=48).dataset()
 
 
-def _run(rank, world, port, route, out):
+def _run(rank, world, init, route, out):
     from musicrecommendation_amd.sharding import EnsembleScorer
 
     if world > 1:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         sc = EnsembleScorer(_dataset(), rank, world, 0, ibm_route=route)
@@ -57,7 +48,7 @@ def test_two_ranks_per_model_layouts_on_one_gpu(route):
     ctx = mp.get_context("spawn")
     with ctx.Manager() as m:
         out = m.dict()
-        mp.start_processes(_run, args=(world, _free_port(), route, out), nprocs=world, join=True,
+        mp.start_processes(_run, args=(world, pg_init_method(), route, out), nprocs=world, join=True,
                            start_method="spawn")
         res = dict(out)
     for name, rows in one_blocks.items():

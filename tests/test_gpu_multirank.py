@@ -3,22 +3,15 @@ rank): the song-sharded layouts end to end with real engine contexts —
 * top-k exchange (all-gather + merge) = the single-context lists;
 * DeviceEnsemble: per-shard combinations = the full model's columns, and the
   threshold mAP after the MIN/MAX + SUM reductions = the single-context value."""
-import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+from helpers import pg_init_method
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _dataset():
@@ -26,10 +19,8 @@ def _dataset():
     return synth.config("c2", n_test=16).dataset()
 
 
-def _worker(rank, world, port, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, out):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from musicrecommendation_amd import evaluation
         from musicrecommendation_amd.engine import Engine
@@ -64,7 +55,7 @@ def test_two_ranks_song_shards_on_one_gpu():
     ctx = mp.get_context("spawn")
     with ctx.Manager() as m:
         out = m.dict()
-        mp.start_processes(_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_worker, args=(world, pg_init_method(), out), nprocs=world, join=True, start_method="spawn")
         res = dict(out)
     ds = _dataset()
     with Engine(ds, out_dtype="f64", topk=10) as e:

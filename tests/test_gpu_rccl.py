@@ -27,6 +27,7 @@ from musicrecommendation_amd.ensemble import DeviceEnsemble
 from musicrecommendation_amd.sharding import ShardScorer, exchange_topk, merge_gathered_host
 
 from oracle import native
+from helpers import pg_init_method
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,14 +39,27 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _torchrun(args, env, tries=3):
+    """bench.py under torchrun at one rank on a port found free just before.
+    Another process can take that port before torchrun's store binds it
+    (EADDRINUSE at the rendezvous, before any GPU work): then a fresh port."""
+    for _ in range(tries):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+               *args]
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+        if p.returncode == 0 or "EADDRINUSE" not in p.stderr:
+            return p
+    return p
+
+
 @pytest.fixture
-def rccl_group(monkeypatch):
-    """A one-rank RCCL group on cuda:0, as bench.py main() creates it (the
-    rendezvous variables are undone at teardown)."""
-    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
-    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+def rccl_group():
+    """A one-rank RCCL group on cuda:0, as bench.py main() creates it
+    (`device_id`), with a FileStore rendezvous (no TCP port to race for)."""
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    dist.init_process_group("nccl", init_method=pg_init_method(), rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
         yield
@@ -130,11 +144,8 @@ def test_bench_one_rank_rccl_rehearsal(tmp_path):
     barriers, MAX/SUM all-reduces and the forced all-gather exchange, all over
     RCCL (the north star on the 10k/1k C3 shape to keep the test short)."""
     env = dict(os.environ, MR_BENCH_PG="1", TMPDIR=str(tmp_path), PYTHONUNBUFFERED="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "1", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-e2e",
-           "--ns-config", "c3", "--ns-steps", "3", "--ns-warmup", "1"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    p = _torchrun(["--gpus", "1", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--no-e2e",
+                   "--ns-config", "c3", "--ns-steps", "3", "--ns-warmup", "1"], env)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
@@ -156,10 +167,8 @@ def test_bench_c5_one_rank_rccl_rehearsal(tmp_path):
     models' extremes and class-count block over RCCL — the same five mAPs
     as the single-process line computes without collectives."""
     env = dict(os.environ, MR_BENCH_PG="1", TMPDIR=str(tmp_path), PYTHONUNBUFFERED="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "1", "--config", "c5", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-e2e"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    p = _torchrun(["--gpus", "1", "--config", "c5", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+                   "--no-e2e"], env)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]

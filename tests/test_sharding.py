@@ -4,7 +4,6 @@ unsharded result. Per-shard partials come from the fixed-point oracle here
 (no GPU); on the GPU box the same exchange runs over RCCL on engine outputs
 (tests/test_gpu_parity.py::test_song_shards_merge_identical, bench --shard songs)."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -15,6 +14,7 @@ import torch.multiprocessing as mp
 from musicrecommendation_amd import synth
 from musicrecommendation_amd.sharding import exchange_topk, merge_gathered_host, song_shards, user_blocks
 from oracle import native
+from helpers import pg_init_method
 
 
 def test_song_shards_cover_and_balance():
@@ -33,16 +33,8 @@ def test_user_blocks_partition():
     assert user_blocks(8, 8) == [(i, i + 1) for i in range(8)]
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def _worker(rank, world, port, model, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, model, out):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         ds = synth.config("small").dataset()
         lo, hi = song_shards(ds, world)[rank]
@@ -59,7 +51,7 @@ def test_gloo_world2_song_shard_exchange(model):
     world = 2
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, _free_port(), model, out), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, pg_init_method(), model, out), nprocs=world, join=True)
         res = dict(out)
     ds = synth.config("small").dataset()
     _, ts, tk = native.fp_model(ds, model, k=10, dense=False)
@@ -78,13 +70,11 @@ def test_layout_2d():
         layout_2d(6, 4)
 
 
-def _worker_2d(rank, world, port, song_groups, model, out):
+def _worker_2d(rank, world, init, song_groups, model, out):
     """A rank of the 2-D layout with the oracle standing in for the engine:
     its (user block, song shard) cell's top-k, the all-gather inside the
     block's process group, the merge."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         from musicrecommendation_amd.sharding import block_group, layout_2d
 
@@ -107,7 +97,7 @@ def test_gloo_2d_layout_exchange(world, song_groups):
     model = "ibm"
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker_2d, args=(world, _free_port(), song_groups, model, out), nprocs=world, join=True)
+        mp.spawn(_worker_2d, args=(world, pg_init_method(), song_groups, model, out), nprocs=world, join=True)
         res = dict(out)
     ds = synth.config("small").dataset()
     _, ts, tk = native.fp_model(ds, model, k=10, dense=False)
@@ -119,12 +109,10 @@ def test_gloo_2d_layout_exchange(world, song_groups):
     assert covered.all()
 
 
-def _worker_shared(rank, world, port, out):
+def _worker_shared(rank, world, init, out):
     """bench.shared_bulk_dataset: rank 0 builds the dataset once, the others
     load its arrays after a barrier; the node-local file is removed."""
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         import bench
 
@@ -140,7 +128,7 @@ def test_gloo_world2_shared_bulk_dataset(tmp_path, monkeypatch):
     world = 2
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker_shared, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_worker_shared, args=(world, pg_init_method(), out), nprocs=world, join=True)
         res = dict(out)
     ds = synth.config("small").dataset()
     for r in range(world):
