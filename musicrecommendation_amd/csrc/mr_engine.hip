@@ -842,7 +842,7 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
                                                 int* s_pre, int* s_scan, Add add, Mark mark, bool ranged = false,
                                                 int v0 = 0, int v1 = 0, const int* sbound = nullptr,
                                                 int chunk_idx = 0, int nc1 = 0, const int2* te_rng = nullptr,
-                                                const long long* te_q = nullptr) {
+                                                const long long* te_q = nullptr, long long* sb = nullptr) {
   const int tid = threadIdx.x;
   for (long long base = t0; base < t1; base += kThreads) {
     const int n = (int)min((long long)kThreads, t1 - base);
@@ -878,6 +878,7 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
     s_pre[tid] = pre;
     if (tid == 0) s_pre[kThreads] = total;
     __syncthreads();
+    stamp_at(sb, 10);  // (diagnostic build) the batch's songs resolved and scanned
     // 16 flattened entries per thread in flight: the listener loads of one
     // batch are issued together, then their accumulations.
     // Segment search (j with s_pre[j] <= i < s_pre[j+1]): groups of 4
@@ -946,6 +947,7 @@ __device__ __forceinline__ void walk_neighbours(long long t0, long long t1, cons
       for (int r = 0; r < 16; ++r)
         if (v[r] >= 0) add(v[r], wv[r]);
     }
+    stamp_at(sb, 11);  // (diagnostic build) thread 0's searches, listener loads and adds issued
     __syncthreads();
   }
 }
@@ -959,14 +961,14 @@ __device__ __forceinline__ void accumulate_neighbours(unsigned long long* Y, lon
                                                       unsigned* heard, int blo, int bhi, bool ranged = false,
                                                       int v0 = 0, int v1 = 0, const int* sbound = nullptr,
                                                       int chunk_idx = 0, int nc1 = 0, const int2* te_rng = nullptr,
-                                                      const long long* te_q = nullptr) {
+                                                      const long long* te_q = nullptr, long long* sb = nullptr) {
   walk_neighbours<MODEL>(
       t0, t1, te_songs, trs_off, trs_users, q_song, s_lo, s_w, s_pre, s_scan,
       [&](int v, unsigned long long w) { atomicAdd(&Y[v - v0], w); },
       [&](int s2) {
         if (heard && s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
       },
-      ranged, v0, v1, sbound, chunk_idx, nc1, te_rng, te_q);
+      ranged, v0, v1, sbound, chunk_idx, nc1, te_rng, te_q, sb);
 }
 
 // Neighbour weight from the stage-1 sum: ibm uses it as is; ubm turns the
@@ -1042,6 +1044,13 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
 // stage 2 (+ fused stage 1, + stage 3): one workgroup per (song tile, test
 // user). MR:159-166 (ubm rank), MR:249-257 (ibm rank), MR:105-111 (pairs).
 // ---------------------------------------------------------------------------
+#ifndef MR_COUNTER_STRIDE
+#define MR_COUNTER_STRIDE 64  // words between two users' hand-off counters: one 256-B line each.
+                              // Every tile's agent-scope add on its user's counter is a memory-side
+                              // atomic; packed (1), the 220 adds of a C2 step hit one line and
+                              // serialise: 12.20-12.23 vs 11.95-11.99 us per step (profiles/r06/s29-s30)
+#endif
+constexpr int kCounterStride = MR_COUNTER_STRIDE;
 struct ScoreParams {
   int n_tr;
   int user0;
@@ -1174,7 +1183,13 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
                                  reinterpret_cast<long long*>(smem_raw + L.s_w),
                                  reinterpret_cast<int*>(smem_raw + L.s_pre),
                                  reinterpret_cast<int*>(smem_raw + L.s_scan), heard, blo, bhi, false, 0, 0,
-                                 nullptr, 0, 0, p.te_rng, p.te_q);
+                                 nullptr, 0, 0, p.te_rng, p.te_q,
+#ifdef MR_STAMPS
+                                 sb
+#else
+                                 nullptr
+#endif
+    );
     MR_STAMP(1);
     if (MODEL == MR_UBM) {  // overlap counts -> fixed-point cosines (MR:142-148), in place
       const double rs_u = p.sqrt_te[u];
@@ -1436,7 +1451,8 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(&p.counter[u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(&p.counter[(size_t)u * kCounterStride], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
     *flag = (old == (unsigned)(p.n_tiles - 1));
   }
   __syncthreads();
@@ -1556,7 +1572,7 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       p.top_song[o] = fs[r];
       p.top_score[o] = fk[r] >= 0 ? __longlong_as_double(fk[r]) : (double)NAN;
     }
-  if (tid == 0) p.counter[u] = 0u;  // ready for the next launch (kernel boundary orders it)
+  if (tid == 0) p.counter[(size_t)u * kCounterStride] = 0u;  // ready for the next launch (kernel boundary orders it)
   MR_STAMP(9);
 }
 
@@ -4850,8 +4866,10 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     c->top_song.n = nk;
     c->top_song.own = false;
     if ((rc = dev_alloc(c->top_score, (size_t)n_te * k))) return rc;
-    if ((rc = dev_alloc(c->counter, (size_t)n_te))) return rc;
-    MR_HIP(hipMemsetAsync(c->counter.p, 0, (size_t)n_te * sizeof(unsigned), st));
+    // (the in-launch hand-off's per-user counters, one line each: fused / separate shapes only)
+    const size_t n_ctr = wide ? (size_t)n_te : (size_t)n_te * kCounterStride;
+    if ((rc = dev_alloc(c->counter, n_ctr))) return rc;
+    MR_HIP(hipMemsetAsync(c->counter.p, 0, n_ctr * sizeof(unsigned), st));
   }
   const size_t esz = c->opt.out_dtype == MR_OUT_F64 ? 8 : 4;
   if ((rc = dev_alloc(c->dense, c->opt.dense ? (size_t)n_te * width * esz : 1))) return rc;

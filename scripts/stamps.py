@@ -45,6 +45,10 @@ def phase(name, a, b, rows=None):
 
 
 phase("stage1", 0, 1)
+if e.fused and (full[:, 10] != 0).all() and (full[:, 11] != 0).all():  # fused stage-1 sub-phases
+    phase("  songs+scan", 0, 10)
+    phase("  search+loads+adds", 10, 11)
+    phase("  barrier wait+weights", 11, 1)
 phase("stage2", 1, 2)
 phase("epilogue", 2, 3)
 phase("tile-topk", 3, 4)
@@ -63,6 +67,7 @@ lu = np.where(last)[0]
 print("last-WG merge start (us) per user:", np.round(rt[lu, 5] - t0, 2).tolist())
 if e.fused and e.shape == "fused":
     nt = e.n_tiles
-    for name, a, b in (("stage1", 0, 1), ("stage2", 1, 2), ("start", None, 0)):
+    sub = (("s1 songs", 0, 10), ("s1 gather", 10, 11), ("s1 tail", 11, 1)) if (full[:, 10] != 0).all() else ()
+    for name, a, b in (("stage1", 0, 1), *sub, ("stage2", 1, 2), ("start", None, 0)):
         d = (rt[:, b] - (rt[:, a] if a is not None else t0)).reshape(-1, nt)
-        print(f"per-user {name:6s} med/max us:", [(round(float(np.median(r)), 2), round(float(r.max()), 2)) for r in d])
+        print(f"per-user {name:9s} med/max us:", [(round(float(np.median(r)), 2), round(float(r.max()), 2)) for r in d])
