@@ -1044,6 +1044,13 @@ __global__ __launch_bounds__(kThreads) void k_neighbours(NbrParams p) {
 // stage 2 (+ fused stage 1, + stage 3): one workgroup per (song tile, test
 // user). MR:159-166 (ubm rank), MR:249-257 (ibm rank), MR:105-111 (pairs).
 // ---------------------------------------------------------------------------
+#ifndef MR_FUSED_SCHED
+#define MR_FUSED_SCHED 1  // fused stage 1 from mr_load's walk schedule (0: the per-step segment search)
+#endif
+#ifndef MR_SCHED_SE
+#define MR_SCHED_SE 8     // fused stage 1: schedule entries per thread per batch (C2 per step: 4 9.92-10.00,
+                          // 6 10.26-10.33, 8 9.93-9.95, 12 10.27-10.30, 16 10.99-11.02 us; profiles/r06/s33-s34)
+#endif
 #ifndef MR_COUNTER_STRIDE
 #define MR_COUNTER_STRIDE 64  // words between two users' hand-off counters: one 256-B line each.
                               // Every tile's agent-scope add on its user's counter is a memory-side
@@ -1065,6 +1072,11 @@ struct ScoreParams {
   const unsigned* tpack;         // fused shape: the same entries as (train user << 16) | tile-local song
   const int2* te_rng;            // fused shape: per te_songs entry, (trs_off[s2], c_tr(s2))
   const long long* te_q;         // fused shape: per te_songs entry, q_song[s2]
+  // fused shape: stage 1's walk schedule (mr_load) — per test user, one entry
+  // per (song of T(u), listener) in song order: (trs_users index, song's slot
+  // in T(u)); sched_off[u] .. sched_off[u + 1]. Null: the in-kernel search.
+  const uint2* te_sched;
+  const long long* sched_off;
   const double* sqrt_c;          // sqrt(c(s)) (train+test, dups), MR:237
   // fused stage 1 inputs
   const long long* trs_off;
@@ -1145,6 +1157,27 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
   for (int i = tid; i < bw; i += kThreads) acc[i] = 0ull;
   for (int i = tid; i < bs / 32; i += kThreads) heard[i] = 0u;
   const long long t0 = p.te_off[u], t1 = p.te_off[u + 1];
+  // Fused stage 1 from the walk schedule: its first loads (this thread's
+  // first song of T(u) for the heard bitmap, its first kSE schedule entries)
+  // are issued before every prefetch below — the vector-memory counter
+  // retires loads in issue order, so waiting on them then does not wait on
+  // the prefetches issued after them. (Unconditional loads at clamped
+  // indices, validity re-derived from the index at use: a predicated load
+  // compiles to a branch with a full wait.)
+  const bool sched = FUSED && p.te_sched != nullptr;
+  constexpr int kSE = MR_SCHED_SE;  // schedule entries per thread in flight
+  long long se0 = 0, se1 = 0;
+  int hs0 = -1;
+  uint2 sc1[kSE];
+  if (sched) {
+    se0 = p.sched_off[u];
+    se1 = p.sched_off[u + 1];
+    if (t1 > t0) hs0 = p.te_songs[min(t0 + tid, t1 - 1)];  // (block-uniform guards: an empty user reads nothing)
+    if (se1 > se0) {
+#pragma unroll
+      for (int r = 0; r < kSE; ++r) sc1[r] = p.te_sched[min(se0 + tid + (long long)r * kThreads, se1 - 1)];
+    }
+  }
   // Prefetch this thread's epilogue scales (hidden behind stages 1-2): songs
   // tid + 256 j of the tile, j < kFusedPre (the whole tile up to 1024 songs).
   double sc[kFusedPre];
@@ -1176,8 +1209,50 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       str[r] = (MODEL == MR_UBM && v < p.n_tr) ? p.sqrt_tr[v] : 1.0;
     }
     unsigned long long* Y = reinterpret_cast<unsigned long long*>(smem_raw + L.y);
+    int v[kSE];
+    unsigned long long wv[kSE];
+    auto gather = [&]() {  // (clamped entries are real ones: loads always in bounds)
+#pragma unroll
+      for (int r = 0; r < kSE; ++r) {
+        v[r] = p.trs_users[sc1[r].x];
+        wv[r] = (MODEL == MR_IBM) ? (unsigned long long)p.te_q[t0 + sc1[r].y] : 1ull;
+      }
+    };
+    const bool any = sched && se1 > se0;  // (block-uniform: a user without entries gathers nothing)
     for (int i = tid; i < p.n_tr; i += kThreads) Y[i] = 0ull;
     __syncthreads();
+    if (sched) {
+      // Stage 1 from the walk schedule: every (song of T(u), listener) entry
+      // names its trs_users index and its song's slot in T(u), so the entries
+      // are loaded coalesced (the first kSE per thread above), with no
+      // per-step prefix scan, barrier or segment search before the listener
+      // gather; the gather (trs_users) and the Y adds are this step's work.
+      if (any) gather();  // (issued before the zeroing barrier instead: slower, profiles/r06/s33)
+      // the tile's heard songs, after the first gather is issued (their
+      // wait then covers loads the adds need next anyway)
+      auto mark = [&](int s2) {
+        if (s2 >= blo && s2 < bhi) atomicOr(&heard[(s2 - blo) >> 5], 1u << ((s2 - blo) & 31));
+      };
+      if (t0 + tid < t1) mark(hs0);
+      for (long long i = t0 + tid + kThreads; i < t1; i += kThreads) mark(p.te_songs[i]);  // |T(u)| > 256
+#ifdef MR_STAMPS
+      stamp_at(sb, 10);
+#endif
+      for (long long i0 = se0 + tid; any;) {
+#pragma unroll
+        for (int r = 0; r < kSE; ++r)
+          if (i0 + (long long)r * kThreads < se1) atomicAdd(&Y[v[r]], wv[r]);
+        i0 += (long long)kSE * kThreads;
+        if (i0 >= se1) break;  // (users with more than kSE x 256 entries: the next batch)
+#pragma unroll
+        for (int r = 0; r < kSE; ++r) sc1[r] = p.te_sched[min(i0 + (long long)r * kThreads, se1 - 1)];
+        gather();
+      }
+#ifdef MR_STAMPS
+      stamp_at(sb, 11);
+#endif
+      __syncthreads();
+    } else
     accumulate_neighbours<MODEL>(Y, t0, t1, p.te_songs, p.trs_off, p.trs_users, p.q_song,
                                  reinterpret_cast<long long*>(smem_raw + L.s_lo),
                                  reinterpret_cast<long long*>(smem_raw + L.s_w),
@@ -3781,6 +3856,8 @@ struct mr_ctx {
   DevBuf<unsigned> tpack;  // fused shape: tile entries as (train user << 16) | tile-local song
   DevBuf<int2> te_rng;     // fused shape: listener range of every test-visible song
   DevBuf<long long> te_q;  // fused shape: its ibm weight q_song
+  DevBuf<uint2> te_sched;  // fused shape: stage 1's walk schedule (ScoreParams::te_sched)
+  DevBuf<long long> sched_off;
   DevBuf<int> sbound;  // stage-1 chunk boundaries of every listener list (n_chunks > 1)
   DevBuf<unsigned> counter;
   DevBuf<double> sqrt_c, sqrt_tr, sqrt_te, top_score;
@@ -3854,7 +3931,7 @@ struct mr_ctx {
   void release_data() {
     tr_off.release(); te_off.release(); trs_off.release(); q_song.release();
     cand_key.release(); top_key.release(); nbr_q.release();
-    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
+    tsongs.release(); tpack.release(); te_rng.release(); te_q.release(); te_sched.release(); sched_off.release(); te_songs.release(); trs_users.release(); toff.release(); sbound.release();
     nbr_v.release(); nbr_cnt.release(); cand_song.release(); top_song.release();
     counter.release();
     sqrt_c.release(); sqrt_tr.release(); sqrt_te.release(); top_score.release();
@@ -4763,6 +4840,28 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
     }
     if ((rc = dev_upload(c->te_rng, rng.data(), rng.size(), st))) return rc;
     if ((rc = dev_upload(c->te_q, tq.data(), tq.size(), st))) return rc;
+    // Stage 1's walk schedule: per test user, its (song, listener) entries in
+    // song order as (trs_users index, slot of the song in T(u)) — the segment
+    // each flattened entry falls in, which the kernel otherwise finds per step
+    // by a prefix scan and a binary search. Index metadata like te_rng (it
+    // names positions, not listener ids or weights); skipped past 2^26 entries.
+    std::vector<long long> h_sched_off((size_t)n_te + 1, 0);
+    for (int u = 0; u < n_te; ++u) {
+      long long n = 0;
+      for (long long i = d->te_off[u]; i < d->te_off[u + 1]; ++i) n += rng[(size_t)i].y;
+      h_sched_off[(size_t)u + 1] = h_sched_off[(size_t)u] + n;
+    }
+    const long long n_sched = h_sched_off[(size_t)n_te];
+    if (MR_FUSED_SCHED && n_sched <= (1ll << 26)) {
+      std::vector<uint2> sched(std::max<long long>(1, n_sched));
+      size_t o = 0;
+      for (int u = 0; u < n_te; ++u)
+        for (long long i = d->te_off[u]; i < d->te_off[u + 1]; ++i)
+          for (int e = 0; e < rng[(size_t)i].y; ++e)
+            sched[o++] = make_uint2((unsigned)(rng[(size_t)i].x + e), (unsigned)(i - d->te_off[u]));
+      if ((rc = dev_upload(c->te_sched, sched.data(), sched.size(), st))) return rc;
+      if ((rc = dev_upload(c->sched_off, h_sched_off.data(), h_sched_off.size(), st))) return rc;
+    }
   }  // (separate / wide shapes: neighbour lists allocated by the first two-hop run, ensure_nbr)
   if (route == 2) {
     const size_t nr = row_song.size();
@@ -5336,6 +5435,7 @@ int run_model(mr_ctx* c, int model) {
       sp.te_off = c->te_off.p; sp.te_songs = c->te_songs.p;
       sp.toff = c->toff.p; sp.tsongs = c->tsongs.p; sp.tpack = c->tpack.p; sp.sqrt_c = c->sqrt_c.p;
       sp.te_rng = c->te_rng.p; sp.te_q = c->te_q.p;  // fused shape (else null)
+      sp.te_sched = c->te_sched.p; sp.sched_off = c->sched_off.p;
 #ifdef MR_NO_TERNG  // A/B experiments: stage 1 looks the listener ranges up itself
       sp.te_rng = nullptr;
 #endif

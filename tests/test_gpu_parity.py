@@ -72,6 +72,28 @@ def test_golden_fixture(name, model):
     assert rel_err(g32, z[model]) < 1e-5
 
 
+@pytest.mark.parametrize("model", MODELS)
+def test_fused_walk_schedule_batches(model):
+    """The fused shape's stage 1 reads mr_load's walk schedule in batches of
+    MR_SCHED_SE entries per thread: a test user with ~25k (song, listener)
+    entries takes a dozen batches and has more than 256 visible songs (the
+    heard-song tail loop); one whose visible songs no train user heard has no
+    entry at all. Bitwise against the fixed-point oracle, k = 1 and 10."""
+    rng = np.random.default_rng(7)
+    train = []
+    for v in range(700):
+        songs = set(range(40)) if v < 600 else set()
+        songs |= set(rng.choice(np.arange(40, 2000), size=20, replace=False).tolist())
+        train += [f"t{v:04d}\ts{s:04d}\t1" for s in sorted(songs)]
+    test = [f"H\ts{s:04d}\t1" for s in range(300)]
+    test += [f"E\tx{j}\t1" for j in range(5)]
+    test += [f"N\ts{int(s):04d}\t1" for s in rng.choice(2000, 30, replace=False)]
+    labels = ["H\ts0500\t1", "E\ts0001\t1", "N\ts0002\t1"]
+    ds = dataset_from_lines(train, test, labels)
+    for k in (1, 10):
+        check_exact(ds, model, k=k, stage1="fused")
+
+
 @pytest.mark.parametrize("stage1", ["fused", "separate"])
 @pytest.mark.parametrize("block", [256, 512, 768, 1024, 2048, 8192, 16384])
 @pytest.mark.parametrize("model", MODELS)
