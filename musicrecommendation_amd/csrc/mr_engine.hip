@@ -4058,6 +4058,12 @@ bool cooc_light_opt() {
   const char* e = std::getenv("MR_COOC_LIGHT");
   return !(e && std::atoi(e) == 0);
 }
+// fused stage 1 from the load-time walk schedule (MR_FUSED_SCHED=0 at load:
+// the per-step segment search, as past the schedule's size cap)
+bool fused_sched_opt() {
+  const char* e = std::getenv("MR_FUSED_SCHED");
+  return MR_FUSED_SCHED && !(e && std::atoi(e) == 0);
+}
 // Heavy u16 rows by tile groups (k_cooc_group, default) or per tile
 // (MR_COOC_GROUP=0: k_cooc_build<512, true>; A/B experiments and tests; read
 // at each mr_load).
@@ -4852,7 +4858,7 @@ int mr_load(mr_ctx* c, const mr_dataset* d) {
       h_sched_off[(size_t)u + 1] = h_sched_off[(size_t)u] + n;
     }
     const long long n_sched = h_sched_off[(size_t)n_te];
-    if (MR_FUSED_SCHED && n_sched <= (1ll << 26)) {
+    if (fused_sched_opt() && n_sched <= (1ll << 26)) {
       std::vector<uint2> sched(std::max<long long>(1, n_sched));
       size_t o = 0;
       for (int u = 0; u < n_te; ++u)

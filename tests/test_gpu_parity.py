@@ -72,13 +72,18 @@ def test_golden_fixture(name, model):
     assert rel_err(g32, z[model]) < 1e-5
 
 
+@pytest.mark.parametrize("sched", ["1", "0"])
 @pytest.mark.parametrize("model", MODELS)
-def test_fused_walk_schedule_batches(model):
+def test_fused_walk_schedule_batches(model, sched, monkeypatch):
     """The fused shape's stage 1 reads mr_load's walk schedule in batches of
     MR_SCHED_SE entries per thread: a test user with ~25k (song, listener)
     entries takes a dozen batches and has more than 256 visible songs (the
     heard-song tail loop); one whose visible songs no train user heard has no
-    entry at all. Bitwise against the fixed-point oracle, k = 1 and 10."""
+    entry at all. MR_FUSED_SCHED=0 (read by mr_load): the per-step segment
+    search that runs past the schedule's size cap. Bitwise against the
+    fixed-point oracle, k = 1 and 10, and C2 on both paths."""
+    monkeypatch.setenv("MR_FUSED_SCHED", sched)
+    check_exact(synth.config("c2").dataset(), model, stage1="fused")
     rng = np.random.default_rng(7)
     train = []
     for v in range(700):
