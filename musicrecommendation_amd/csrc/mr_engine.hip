@@ -624,6 +624,20 @@ __device__ __forceinline__ int tile_of(int key, int bs, float inv_bs) {
   return t;
 }
 
+// Comparisons per thread past which rank_survivors hands its candidates to one
+// wave (k rounds of a wave-wide best) instead of ranking them all at once. The
+// fused shape's 256 threads rank up to 128 survivors themselves: a UserBasedModel
+// tile with many equal scores at tau (C1) otherwise spent ~4 us in the one-wave
+// select — C1 15.0 -> 10.5 us per step, C2 unchanged (profiles/r06/s47).
+#ifndef MR_RANK_Q_FUSED
+#define MR_RANK_Q_FUSED 64
+#endif
+#ifndef MR_RANK_Q_WIDE
+#define MR_RANK_Q_WIDE 16
+#endif
+template <int NT>
+constexpr int kRankQ = NT <= 256 ? MR_RANK_Q_FUSED : MR_RANK_Q_WIDE;
+
 // Ranks of nc <= 256 survivor candidates ck/cs among themselves (total order
 // (key desc, song asc)): rank < k -> output slot; slots past nc get (-1, -1).
 // crank: 256 zeroed ints. All threads call it; it ends with a barrier (not
@@ -632,7 +646,7 @@ template <int NT>
 __device__ __forceinline__ void rank_survivors(int nc, int k, const long long* ck, const int* cs, int* crank,
                                                long long* out_k, int* out_s, const TopkDst& dst = TopkDst{}) {
   const int tid = threadIdx.x, lane = tid & 63;
-  if (nc * nc > 16 * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
+  if (nc * nc > kRankQ<NT> * NT) {  // many ties at tau: one wave selects (4 candidates per lane)
     if (tid < 64) {
       long long rk[4];
       int rs[4];
