@@ -635,6 +635,9 @@ __device__ __forceinline__ int tile_of(int key, int bs, float inv_bs) {
 #ifndef MR_RANK_Q_WIDE
 #define MR_RANK_Q_WIDE 16
 #endif
+#ifndef MR_MERGE_INTERLEAVE
+#define MR_MERGE_INTERLEAVE 1  // C2 9.84-9.88 vs 9.91-9.93 us per step, profiles/r06/s54
+#endif
 #ifndef MR_RANK_UNROLL_FUSED
 #define MR_RANK_UNROLL_FUSED 4
 #endif
@@ -1595,8 +1598,15 @@ __global__ __launch_bounds__(kThreads) void k_score(ScoreParams p) {
       long long rk = kKeyNone;
       int rs = INT_MAX;
       if (tid < nck) {
-        rk = ld_sc1(&ck[tid]);
-        rs = ld_sc1(&cs[tid]);
+#if MR_MERGE_INTERLEAVE
+        // thread t holds position t / n_tiles of tile t % n_tiles: a threshold
+        // row is one list position over 8 tiles, not 8 positions of one tile
+        const int ci = (tid % p.n_tiles) * k + tid / p.n_tiles;
+#else
+        const int ci = tid;
+#endif
+        rk = ld_sc1(&ck[ci]);
+        rs = ld_sc1(&cs[ci]);
       }
       MR_STAMP(6);
       auto get_r = [&](int, long long& key, int& song) { key = rk; song = rs; };  // called for i = tid only
